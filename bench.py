@@ -1,0 +1,263 @@
+"""Benchmark: NetRep permutation null distributions on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's "20k genes x 50 modules"):
+synthetic coexpression, 20,000 genes x 500 samples, 50 modules of
+round(linspace(30, 300, 50)) genes, null = "overlap", all seven statistics.
+A step = one batch of --batch permutations (every module of each) through
+the engine, nulls copied back to host memory. Inputs (test corr, net, scaled
+data, discovery vectors) are resident in HBM before the timed region.
+
+Multi-GPU: one process per GPU (torchrun). Rank 0 builds the datasets and
+broadcasts the test matrices over RCCL; every rank then evaluates its own
+disjoint permutation range (weak scaling: fixed permutations per GPU), with
+no collective on the data path. Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import netrep_amd as N  # noqa: E402
+from netrep_amd import synthetic as S  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_MFMA_PEAK_TFS = 78.6    # MI355X fp64 matrix peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=256, help="permutations per step")
+    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4"])
+    ap.add_argument("--cpu-baseline-perms", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def scale_rows(x):
+    """Scale (src/scale.cpp:21) applied to genes stored as rows of x (N x S)."""
+    mu = x.mean(dim=1, keepdim=True)
+    sd = x.std(dim=1, unbiased=True, keepdim=True)
+    return (x - mu) / sd
+
+
+def build_case(cfg, world, rank, local, seed):
+    n_nodes, n_samples, sizes, _, with_data = S.CONFIGS[cfg]
+    lay = S.make_layout(n_nodes, sizes, seed)
+    dev = torch.device("cuda", local)
+    eng = N.Engine(local)
+    mods = lay.modules
+    node_off = np.concatenate([[0], np.cumsum([lay.members[m].size for m in mods])]).astype(np.int64)
+    idx = np.concatenate([lay.members[m] for m in mods]).astype(np.int32)
+    # -- discovery vectors (IntermediateProperties on the device), rank 0 then broadcast
+    k = np.diff(node_off)
+    n_cv = int((k * (k - 1) // 2).sum())
+    vec = torch.empty(n_cv + 2 * int(node_off[-1]), dtype=torch.float64, device=dev)
+    if rank == 0:
+        dx, dc, dn = S.torch_dataset(lay, n_samples, seed + 1, device=dev)
+        dxs = scale_rows(dx).contiguous()
+        eng.set_dataset_device(dc.data_ptr(), dn.data_ptr(), dxs.data_ptr() if with_data else 0,
+                               n_nodes, n_samples)
+        del dx, dc, dn, dxs
+        torch.cuda.empty_cache()
+        v = eng.module_vectors(node_off, idx, with_data)
+        parts = [v["corr"], v["degree"], v["contribution"] if with_data else np.zeros(int(node_off[-1]))]
+        vec.copy_(torch.from_numpy(np.concatenate(parts)))
+    if world > 1:
+        dist.broadcast(vec, src=0)
+    v = vec.cpu().numpy()
+    disc_cv, disc_wd, disc_nc = v[:n_cv], v[n_cv:n_cv + node_off[-1]], v[n_cv + node_off[-1]:]
+    # -- test dataset: built on rank 0, broadcast over RCCL (xGMI) to every rank
+    if rank == 0:
+        tx, tc, tn = S.torch_dataset(lay, n_samples, seed + 2, preserve_all=False, device=dev)
+        txs = scale_rows(tx).contiguous()
+        del tx
+    else:
+        txs = torch.empty((n_nodes, n_samples), dtype=torch.float64, device=dev)
+        tc = torch.empty((n_nodes, n_nodes), dtype=torch.float64, device=dev)
+        tn = torch.empty((n_nodes, n_nodes), dtype=torch.float64, device=dev)
+    t_bcast = 0.0
+    if world > 1:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in (tc, tn, txs):
+            dist.broadcast(t, src=0)
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - t0
+    eng.set_dataset_device(tc.data_ptr(), tn.data_ptr(), txs.data_ptr() if with_data else 0,
+                           n_nodes, n_samples)
+    eng.set_modules(len(mods), np.arange(len(mods)), node_off, idx, idx,  # null pool = all genes
+                    disc_cv, disc_wd, disc_nc if with_data else None)
+    eng.set_null_pool(np.arange(n_nodes, dtype=np.int32))
+    host = None
+    if rank == 0 and world == 1:
+        host = dict(tc=tc, tn=tn, txs=txs)  # kept for the CPU baseline sample
+    else:
+        del tc, tn, txs
+    torch.cuda.empty_cache()
+    return eng, lay, dict(node_off=node_off, idx=idx, disc_cv=disc_cv, disc_wd=disc_wd,
+                          disc_nc=disc_nc, with_data=with_data, n_samples=n_samples,
+                          n_nodes=n_nodes, t_bcast=t_bcast), host
+
+
+def roofline_terms(sizes, n_samples, with_data):
+    """Algorithmic bytes / flops per permutation, per kernel."""
+    k = np.asarray(sizes, dtype=np.float64)
+    net_bytes = (4 * k + 8 * k * (k - 1) / 2 + 8 * k * k).sum()
+    prof_bytes = (4 * k + 8 * n_samples * k).sum() if with_data else 0.0
+    prof_flops = (2 * n_samples * k * np.minimum(n_samples, k)).sum() if with_data else 0.0
+    return net_bytes, prof_bytes, prof_flops
+
+
+def cpu_baseline(lay, meta, host, n_perm, seed):
+    """Oracle (numpy/scipy restatement of the reference's CPU path) on a bounded
+    sample of the same workload, single thread."""
+    sys.path.insert(0, ROOT)
+    from oracle import netrep_oracle as O
+    from oracle import prp
+    tc = host["tc"].cpu().numpy()
+    tn = host["tn"].cpu().numpy()
+    tx = host["txs"].cpu().numpy().T.copy()  # S x N
+    mods = lay.modules
+    mi = O.ModuleIndex(lay.names, lay.labels, lay.names, mods)
+    no = meta["node_off"]
+    disc = {"corr": {}, "degree": {}, "contribution": {}}
+    cvo = 0
+    for j, m in enumerate(mods):
+        kk = int(no[j + 1] - no[j])
+        disc["corr"][m] = meta["disc_cv"][cvo:cvo + kk * (kk - 1) // 2]
+        disc["degree"][m] = meta["disc_wd"][no[j]:no[j + 1]]
+        disc["contribution"][m] = meta["disc_nc"][no[j]:no[j + 1]]
+        cvo += kk * (kk - 1) // 2
+    nn = mi.null_idx.size
+    pis = np.stack([prp.permute(np.arange(nn), nn, seed, p) for p in range(n_perm)]).astype(np.int64)
+    t0 = time.perf_counter()
+    O.permutation_procedure(disc, tx, tc, tn, mi, pis, with_data=meta["with_data"])
+    dt = time.perf_counter() - t0
+    return n_perm / dt, dt
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    eng, lay, meta, host = build_case(args.config, world, rank, local, args.seed)
+    B, K, W = args.batch, args.steps, args.warmup
+    eng.set_batch(B)
+    net_b, prof_b, prof_f = roofline_terms(lay.module_sizes, meta["n_samples"], meta["with_data"])
+
+    def step(s, base):
+        p0 = base + s * B
+        return eng.run(p0, p0 + B, args.seed)
+
+    base_w = 10**9 + rank * W * B
+    for s in range(W):
+        step(s, base_w)
+    eng.synchronize()
+    eng.set_timing(True)
+    eng.reset_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    base = rank * K * B
+    for s in range(K):
+        nulls = step(s, base)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms0, l0, _ = eng.timing(0)
+    ms1, l1, _ = eng.timing(1)
+    finite = float(np.isfinite(nulls).mean())
+
+    if rank == 0:
+        total_perms = world * K * B
+        value = total_perms / elapsed
+        # dominant kernel + roofline (per launch = one batch of B permutations)
+        kernels = {
+            "module_net_kernel": {"bound": "hbm", "avg_ms": ms0 / max(l0, 1), "launches": l0,
+                                  "achieved": net_b * B / (ms0 / max(l0, 1) / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s"},
+        }
+        if meta["with_data"]:
+            kernels["module_profile_kernel"] = {
+                "bound": "mfma", "avg_ms": ms1 / max(l1, 1), "launches": l1,
+                "achieved": prof_f * B / (ms1 / max(l1, 1) / 1e3) / 1e12, "peak": FP64_MFMA_PEAK_TFS,
+                "unit": "TFLOP/s"}
+        for kv in kernels.values():
+            kv["frac"] = kv["achieved"] / kv["peak"]
+        dom_name = max(kernels, key=lambda n: kernels[n]["avg_ms"])
+        dom = kernels[dom_name]
+        roofline = {"kernel": dom_name, "bound": dom["bound"], "achieved": round(dom["achieved"], 4),
+                    "peak": dom["peak"], "unit": dom["unit"], "frac": round(dom["frac"], 6),
+                    "traffic": None}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and host is not None:
+            rate, dt = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)
+            cpu = {"value": rate, "unit": "permutations/sec", "cores": 1, "kind": "port",
+                   "sample": f"{args.cpu_baseline_perms} permutations x 50 modules of the same workload, "
+                             f"numpy/scipy restatement (gesdd SVD), {dt:.1f} s"}
+        line = {
+            "metric": "permutations/sec (whole node), 20k genes x 50 modules",
+            "value": value,
+            "unit": "permutations/sec",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic coexpression (SURVEY.md 8d generator), random module layout",
+            "config": {"workload": f"{args.config}: {meta['n_nodes']} genes x {meta['n_samples']} samples, "
+                                   f"{len(lay.modules)} modules (30-300 genes), null=overlap, "
+                                   f"{'7' if meta['with_data'] else '4'} statistics",
+                       "perms_per_step": B, "global_perms": total_perms, "parallelism": f"perm-shard x{world}"},
+            "module_perms_per_sec": value * len(lay.modules),
+            "algorithmic_GBps": value * (net_b + prof_b) / 1e9,
+            "roofline": roofline,
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+            "finite_fraction": finite,
+            "broadcast_s": meta["t_bcast"],
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,229 @@
+/* netrep_gpu.h -- C ABI of the MI355X NetRep permutation engine.
+ *
+ * Plain pointers and sizes only; no C++ exceptions cross this boundary. All
+ * matrices are R column-major fp64: A(i,j) at i + j*nrow. Every function
+ * returns NR_OK (0) or an NR_ERR_* code; nr_last_error() has the message.
+ *
+ * Two layers:
+ *  1. Engine layer (nr_*): one context per GPU holding ONE dataset resident
+ *     in HBM, as the reference holds one dataset in RAM at a time
+ *     (R/modulePreservation.R:553-620). It replaces the std::thread pool of
+ *     calculateNulls (src/permutations.cpp:39-105, :335-380;
+ *     src/permutationsNoData.cpp:35-89, :305-339) with batched device
+ *     launches, and the Armadillo/LAPACK statistics of src/netStats.cpp with
+ *     HIP kernels.
+ *  2. Reference-interface layer (netrep_*): the eight Rcpp entry points of
+ *     src/RcppExports.cpp:131-146 with the same argument meaning, taking
+ *     names as C strings. An Rcpp glue unpacks SEXPs and
+ *     calls these one-for-one.
+ */
+#ifndef NETREP_GPU_H
+#define NETREP_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NR_OK 0
+#define NR_ERR_HIP 1          /* HIP runtime / launch failure */
+#define NR_ERR_INVALID 2      /* bad argument, shape or missing prerequisite */
+#define NR_ERR_OOM 3          /* device allocation failed */
+#define NR_ERR_UNSUPPORTED 4  /* size beyond an engine limit (e.g. module > NR_MAX_MODULE_NODES) */
+#define NR_ERR_CANCELLED 5    /* nr_cancel() was called during a run */
+#define NR_ERR_NONFINITE 6    /* CheckFinite failure (src/checkFinite.cpp:25-27) */
+
+#define NR_HOST 0
+#define NR_DEVICE 1
+
+#define NR_MAX_MODULE_NODES 2048
+
+/* Statistic slots in the nulls cube (src/permutations.cpp:95-101, :174-177). */
+#define NR_NSTAT_DATA 7
+#define NR_NSTAT_NODATA 4
+
+typedef struct nr_ctx nr_ctx;
+
+/* ---- engine layer ------------------------------------------------------ */
+
+int nr_device_count(int* count);
+int nr_ctx_create(int device, nr_ctx** out);
+void nr_ctx_destroy(nr_ctx* ctx);
+/* Message of the last failing call on ctx (ctx == NULL: last nr_ctx_create failure). */
+const char* nr_last_error(const nr_ctx* ctx);
+
+/* Make one dataset resident: corr, net (n_nodes x n_nodes) and optional data
+ * (n_samples x n_nodes, scaled as by Scale, src/scale.cpp:14-25; NULL for the
+ * network-only path). `where` = NR_HOST or NR_DEVICE (device pointers, e.g.
+ * after an RCCL broadcast). Replaces the previous dataset. The matrices are
+ * stored interleaved as {corr(i,j), net(i,j)} pairs so one 16-byte read serves
+ * CorrVector (src/netStats.cpp:196-201) and WeightedDegree (:135). */
+int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net,
+                   const double* data, int64_t n_nodes, int64_t n_samples, int where);
+
+/* 1 if corr and net of the resident dataset are exactly symmetric. */
+int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric);
+
+/* Module index sets (a4 of SURVEY.md 8) and discovery vectors (a15).
+ *   n_rows      rows of the output cube = length of `modules`
+ *   n_present   modules with >= 1 node in the test dataset (modsPresent,
+ *               src/permutations.cpp:196-201), in `modules` order
+ *   row_of      [n_present] output row of each present module
+ *   node_off    [n_present+1] CSR offsets of module nodes
+ *   test_idx    [node_off[n_present]] column of each node in the resident
+ *               dataset (GetNodeIdx, src/utils.cpp:147-162); used for the
+ *               observed statistics
+ *   null_pos    [same] position of each node in the null pool (MakeNullMap
+ *               nullMap, src/utils.cpp:108-136); may be NULL if no
+ *               permutations will be run
+ *   disc_corr   concatenated discovery CorrVector per module, k(k-1)/2 each
+ *   disc_degree [nodes] discovery weighted degree (node order)
+ *   disc_contrib[nodes] discovery node contribution, NULL for network-only */
+int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present,
+                   const int32_t* row_of, const int64_t* node_off,
+                   const int32_t* test_idx, const int32_t* null_pos,
+                   const double* disc_corr, const double* disc_degree,
+                   const double* disc_contrib);
+
+/* The null pool nullIdx (MakeNullMap, src/utils.cpp:108-136): test columns. */
+int nr_set_null_pool(nr_ctx* ctx, const int32_t* null_idx, int64_t n_null);
+
+/* Observed statistics (src/permutations.cpp:246-285) into observed
+ * [n_rows x n_stat], column-major (R matrix), NA_REAL for absent modules and
+ * non-finite values (src/permutations.cpp:383-384). n_stat = 7 with data,
+ * 4 without. */
+int nr_observed(nr_ctx* ctx, double* observed);
+
+/* Null distributions for global permutations [perm_begin, perm_end).
+ * pi == NULL: permutation p draws pi_p = keyed PRP(seed, p) (prp.h).
+ * pi != NULL: explicit host table [(perm_end-perm_begin) x n_null] of
+ *   null-pool permutations, pi[p][q] = source position (the exported
+ *   shuffles of the reference, src/permutations.cpp:63).
+ * nulls receives (perm_end-perm_begin) slices of n_rows x n_stat, i.e. the
+ * cube layout m + n_rows*s + n_rows*n_stat*p of src/permutations.cpp:55
+ * starting at permutation perm_begin. Host pointer for nr_run, device pointer
+ * for nr_run_device. */
+int nr_run(nr_ctx* ctx, int64_t perm_begin, int64_t perm_end, uint64_t seed,
+           const uint32_t* pi, double* nulls);
+int nr_run_device(nr_ctx* ctx, int64_t perm_begin, int64_t perm_end,
+                  uint64_t seed, const uint32_t* pi_device, double* nulls_device);
+
+/* Host evaluation of the keyed null-pool permutation: out[p - perm_begin][q]
+ * = pi_p(q) for q < n_null (no GPU needed). */
+int nr_prp_table(uint64_t seed, int64_t perm_begin, int64_t perm_end,
+                 int64_t n_null, uint32_t* out);
+
+/* Export the index sets a run would use: test column of every module node of
+ * permutations [perm_begin, perm_end), layout [perm][node] (CSR node order). */
+int nr_export_indices(nr_ctx* ctx, int64_t perm_begin, int64_t perm_end,
+                      uint64_t seed, int32_t* indices);
+
+/* Per-module vectors for explicit index sets on the resident dataset
+ * (IntermediateProperties src/discProps.cpp:92-122, NetProps
+ * src/properties.cpp:152-185): corr_vec (k(k-1)/2 per module), degree (k),
+ * avg_weight (one per module, AverageEdgeWeight src/netStats.cpp:154-162),
+ * contribution (k), summary (n_samples per module) and coherence (one per
+ * module, ModuleCoherence src/netStats.cpp:293-305). Any output may be NULL;
+ * the last three need data. Node order = CSR order of idx. */
+int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off,
+                      const int32_t* idx, double* corr_vec, double* degree,
+                      double* avg_weight, double* contribution, double* summary,
+                      double* coherence);
+
+/* Column scaling (Scale, src/scale.cpp:14-25) on the device. */
+int nr_scale(nr_ctx* ctx, const double* data, int64_t n_samples,
+             int64_t n_nodes, double* scaled);
+
+/* CheckFinite (src/checkFinite.cpp:21-28): *all_finite = 1 or 0. */
+int nr_check_finite(nr_ctx* ctx, const double* mat, int64_t n_elem, int* all_finite);
+
+/* Progress (replaces MonitorProgress, src/thread-utils.cpp:49-82) and
+ * cancellation (replaces the `interrupted` flag, src/permutations.cpp:362);
+ * both are safe to call from another host thread during nr_run. */
+int nr_progress(nr_ctx* ctx, int64_t* done, int64_t* total);
+int nr_cancel(nr_ctx* ctx);
+
+/* Tuning and measurement. */
+int nr_set_batch(nr_ctx* ctx, int64_t perms_per_launch);
+int nr_set_timing(nr_ctx* ctx, int enable);
+/* Accumulated device time (HIP events on the launch stream) per kernel:
+ * kernel 0 = module network statistics, 1 = summary-profile statistics. */
+int nr_get_timing(nr_ctx* ctx, int kernel, double* total_ms, int64_t* launches,
+                  int64_t* items);
+int nr_reset_timing(nr_ctx* ctx);
+int nr_synchronize(nr_ctx* ctx);
+
+/* ---- reference-interface layer ----------------------------------------- */
+/* Names are arrays of NUL-terminated strings. moduleAssignments is the named
+ * character vector as (node names, labels). Per-module discovery vectors are
+ * given in `modules` order ([n_modules] pointers + lengths; NULL/0 for
+ * modules absent from the test dataset). */
+
+typedef struct netrep_disc_props {
+  const double* const* degree;        /* [n_modules] */
+  const int64_t* degree_len;
+  const double* const* corr;
+  const int64_t* corr_len;
+  const double* const* contribution;  /* NULL for the network-only path */
+  const int64_t* contribution_len;
+} netrep_disc_props;
+
+/* PermutationProcedure (src/permutations.cpp:160-166) and
+ * PermutationProcedureNoData (src/permutationsNoData.cpp:140-146, t_data =
+ * NULL). nulls_out [n_modules x n_stat x n_perm], observed_out
+ * [n_modules x n_stat], both column-major, NA-filled. `seed` keys the PRP;
+ * `pi` (optional, [n_perm x n_null]) supplies explicit shuffles. n_cores is
+ * accepted for interface parity; NETREP_NUM_GPUS selects the GPU count. */
+int netrep_PermutationProcedure(
+    const netrep_disc_props* disc_props, const double* t_data,
+    const double* t_corr, const double* t_net, int64_t n_samples,
+    int64_t n_nodes, const char* const* t_names, const char* const* ma_names,
+    const char* const* ma_labels, int64_t n_assign,
+    const char* const* modules, int64_t n_modules, int64_t n_perm,
+    int32_t n_cores, const char* null_hypothesis, int32_t verbose,
+    uint64_t seed, const uint32_t* pi, double* nulls_out, double* observed_out);
+
+/* IntermediateProperties[NoData] (src/discProps.cpp:44-48, :171-175).
+ * Outputs per module in `modules` order, concatenated; lengths written to
+ * *_len (0 for modules absent from the test node list). Buffers must hold
+ * sum(k), sum(k(k-1)/2) and sum(k) doubles (k = module size in discovery). */
+int netrep_IntermediateProperties(
+    const double* d_data, const double* d_corr, const double* d_net,
+    int64_t n_samples, int64_t n_nodes, const char* const* d_names,
+    const char* const* t_node_names, int64_t n_t_nodes,
+    const char* const* ma_names, const char* const* ma_labels,
+    int64_t n_assign, const char* const* modules, int64_t n_modules,
+    double* degree_out, int64_t* degree_len, double* corr_out,
+    int64_t* corr_len, double* contribution_out, int64_t* contribution_len);
+
+/* NetProps[NoData] (src/properties.cpp:41-44, :190-193). data is unscaled
+ * (NetProps scales internally, :49). Per module (in `modules` order) with
+ * k_all = all module nodes in moduleAssignments order: degree[k_all],
+ * contribution[k_all], summary[n_samples], coherence, avg_weight; NA for
+ * absent nodes (:133-139). *_len receive k_all per module. */
+int netrep_NetProps(const double* data, const double* net, int64_t n_samples,
+                    int64_t n_nodes, const char* const* node_names,
+                    const char* const* ma_names, const char* const* ma_labels,
+                    int64_t n_assign, const char* const* modules,
+                    int64_t n_modules, double* degree_out,
+                    double* contribution_out, double* summary_out,
+                    double* coherence_out, double* avg_weight_out,
+                    int64_t* k_all_out);
+
+/* Scale (src/scale.cpp:38-45). */
+int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes,
+                 double* scaled_out);
+
+/* CheckFinite (src/checkFinite.cpp:21-28): NR_ERR_NONFINITE with the
+ * reference's message if any element is NA/NaN/Inf. */
+int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol);
+
+/* Last error of the reference-interface layer (thread-local). */
+const char* netrep_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NETREP_GPU_H */

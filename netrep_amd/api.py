@@ -1,0 +1,275 @@
+"""NetRep's Rcpp entry points, MI355X engine behind them.
+
+Same names, argument meaning and return shapes as the functions registered in
+src/RcppExports.cpp:131-146 (R wrappers R/RcppExports.R:4-35):
+
+    Scale, CheckFinite, IntermediateProperties, IntermediatePropertiesNoData,
+    PermutationProcedure, PermutationProcedureNoData, NetProps, NetPropsNoData
+
+R values map to Python as:
+  * ``NumericMatrix`` with dimnames -> ``RMatrix(values, rownames, colnames)``
+    (``values`` an ``(nrow, ncol)`` array),
+  * named ``CharacterVector`` moduleAssignments -> ``{node name: label}``
+    (insertion order = the R vector's order),
+  * ``List`` -> ``dict``; numeric arrays -> numpy (R's column-major cube layout
+    for ``nulls``).
+Errors raise ``NetRepError`` where the reference raises an R error.
+Each call goes through the C ABI (``netrep_*``) into HIP kernels; nothing is
+computed on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Mapping, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+STATNAMES = ["avg.weight", "coherence", "cor.cor", "cor.degree", "cor.contrib",
+             "avg.cor", "avg.contrib"]                       # src/permutations.cpp:174-177
+STATNAMES_NODATA = ["avg.weight", "cor.cor", "cor.degree", "avg.cor"]  # src/permutationsNoData.cpp:156-158
+
+DEFAULT_SEED = 0x4E65745265703133  # "NetRep13"
+
+
+@dataclass
+class RMatrix:
+    """An R numeric matrix with dimnames."""
+    values: np.ndarray
+    rownames: Optional[Sequence[str]] = None
+    colnames: Optional[Sequence[str]] = None
+
+    @property
+    def f(self) -> np.ndarray:
+        return np.asfortranarray(np.asarray(self.values, dtype=np.float64))
+
+
+def _strv(names: Sequence[str]):
+    enc = [str(n).encode() for n in names]
+    arr = (C.c_char_p * max(len(enc), 1))(*enc)
+    return arr, enc
+
+
+def _assignments(module_assignments):
+    if isinstance(module_assignments, Mapping):
+        items = list(module_assignments.items())
+    else:
+        items = list(module_assignments)
+    names = [str(n) for n, _ in items]
+    labels = [str(lab) for _, lab in items]
+    return names, labels
+
+
+def _dptr(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def Scale(data) -> RMatrix:
+    """Scale (src/scale.cpp:38-45): per-column (x - mean) / sd, keeping dimnames."""
+    m = data if isinstance(data, RMatrix) else RMatrix(np.asarray(data))
+    x = m.f
+    out = np.empty_like(x, order="F")
+    L.check_api(L.load().netrep_Scale(_dptr(x), x.shape[0], x.shape[1], _dptr(out)))
+    return RMatrix(out, m.rownames, m.colnames)
+
+
+def CheckFinite(mat) -> None:
+    """CheckFinite (src/checkFinite.cpp:21-28): raise on any NA/NaN/Inf."""
+    x = (mat.f if isinstance(mat, RMatrix) else np.asfortranarray(np.asarray(mat, dtype=np.float64)))
+    x2 = x.reshape(x.shape[0], -1) if x.ndim > 1 else x.reshape(-1, 1)
+    L.check_api(L.load().netrep_CheckFinite(_dptr(x2), x2.shape[0], x2.shape[1]))
+
+
+def _intermediate(d_data, d_corr, d_net, t_node_names, module_assignments, modules):
+    lib = L.load()
+    names, labels = _assignments(module_assignments)
+    modules = [str(m) for m in modules]
+    d_names = list(d_net.colnames)
+    n = len(d_names)
+    corr = d_corr.f
+    net = d_net.f
+    data = d_data.f if d_data is not None else None
+    s = data.shape[0] if data is not None else 0
+    # upper bounds for the concatenated outputs: module sizes in discovery
+    sizes = {}
+    tset = set(map(str, t_node_names))
+    for nm, lab in zip(names, labels):
+        if nm in tset:
+            sizes[lab] = sizes.get(lab, 0) + 1
+    ks = [sizes.get(m, 0) for m in modules]
+    deg = np.empty(max(sum(ks), 1))
+    cv = np.empty(max(sum(k * (k - 1) // 2 for k in ks), 1))
+    nc = np.empty(max(sum(ks), 1)) if data is not None else None
+    nm_ = len(modules)
+    deg_len = np.zeros(nm_, dtype=np.int64)
+    cv_len = np.zeros(nm_, dtype=np.int64)
+    nc_len = np.zeros(nm_, dtype=np.int64)
+    dn, _k1 = _strv(d_names)
+    tn, _k2 = _strv(t_node_names)
+    an, _k3 = _strv(names)
+    al, _k4 = _strv(labels)
+    mo, _k5 = _strv(modules)
+    i64 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+    L.check_api(lib.netrep_IntermediateProperties(
+        _dptr(data), _dptr(corr), _dptr(net), s, n, dn, tn, len(t_node_names), an, al, len(names),
+        mo, nm_, _dptr(deg), i64(deg_len), _dptr(cv), i64(cv_len), _dptr(nc),
+        i64(nc_len) if nc is not None else None))
+    out = {"degree": {}, "corr": {}}
+    if data is not None:
+        out["contribution"] = {}
+    od = oc = 0
+    for i, m in enumerate(modules):
+        if deg_len[i] == 0:
+            continue                                     # only modsPresent (src/discProps.cpp:123-125)
+        out["degree"][m] = deg[od:od + deg_len[i]].copy()
+        out["corr"][m] = cv[oc:oc + cv_len[i]].copy()
+        if data is not None:
+            out["contribution"][m] = nc[od:od + nc_len[i]].copy()
+        od += deg_len[i]
+        oc += cv_len[i]
+    return out
+
+
+def IntermediateProperties(dData: RMatrix, dCorr: RMatrix, dNet: RMatrix, tNodeNames,
+                           moduleAssignments, modules) -> dict:
+    """IntermediateProperties (src/discProps.cpp:44-132). dData must be scaled."""
+    return _intermediate(dData, dCorr, dNet, list(tNodeNames), moduleAssignments, modules)
+
+
+def IntermediatePropertiesNoData(dCorr: RMatrix, dNet: RMatrix, tNodeNames, moduleAssignments,
+                                 modules) -> dict:
+    """IntermediatePropertiesNoData (src/discProps.cpp:171-244)."""
+    return _intermediate(None, dCorr, dNet, list(tNodeNames), moduleAssignments, modules)
+
+
+def _permutation(disc_props, t_data, t_corr, t_net, module_assignments, modules, n_perm, n_cores,
+                 null_hypothesis, verbose, seed, pi):
+    lib = L.load()
+    names, labels = _assignments(module_assignments)
+    modules = [str(m) for m in modules]
+    with_data = t_data is not None
+    t_names = list(t_net.colnames)
+    n = len(t_names)
+    corr, net = t_corr.f, t_net.f
+    data = t_data.f if with_data else None
+    s = data.shape[0] if with_data else 0
+    nm_ = len(modules)
+    keep = []
+
+    def vecs(key):
+        d = disc_props.get(key, {}) if disc_props is not None else {}
+        ptrs = (C.POINTER(C.c_double) * max(nm_, 1))()
+        lens = np.zeros(max(nm_, 1), dtype=np.int64)
+        for i, m in enumerate(modules):
+            if m in d:
+                v = np.ascontiguousarray(d[m], dtype=np.float64)
+                keep.append(v)
+                ptrs[i] = _dptr(v)
+                lens[i] = v.size
+        keep.append(lens)
+        return ptrs, lens.ctypes.data_as(C.POINTER(C.c_int64))
+
+    dp = L.DiscProps()
+    dp.degree, dp.degree_len = vecs("degree")
+    dp.corr, dp.corr_len = vecs("corr")
+    if with_data:
+        dp.contribution, dp.contribution_len = vecs("contribution")
+    n_stat = 7 if with_data else 4
+    observed = np.empty((nm_, n_stat), order="F")
+    nulls = np.empty((nm_, n_stat, int(n_perm)), order="F") if n_perm > 0 else None
+    pi_arr = None
+    if pi is not None:
+        pi_arr = np.ascontiguousarray(pi, dtype=np.uint32)
+    tn, _k1 = _strv(t_names)
+    an, _k2 = _strv(names)
+    al, _k3 = _strv(labels)
+    mo, _k4 = _strv(modules)
+    L.check_api(lib.netrep_PermutationProcedure(
+        C.byref(dp), _dptr(data), _dptr(corr), _dptr(net), s, n, tn, an, al, len(names), mo, nm_,
+        int(n_perm), int(n_cores), str(null_hypothesis).encode(), int(bool(verbose)),
+        int(seed) & (2**64 - 1), pi_arr.ctypes.data_as(C.POINTER(C.c_uint32)) if pi_arr is not None else None,
+        _dptr(nulls), _dptr(observed)))
+    statnames = STATNAMES if with_data else STATNAMES_NODATA
+    res = {"observed": observed, "observed_dimnames": (modules, statnames)}
+    if n_perm > 0:
+        res["nulls"] = nulls
+        res["nulls_dimnames"] = (modules, statnames, None)  # "permutation.i" left implicit
+    return res
+
+
+def PermutationProcedure(discProps: dict, tData: RMatrix, tCorr: RMatrix, tNet: RMatrix,
+                         moduleAssignments, modules, nPermutations: int, nCores: int = 1,
+                         nullHypothesis: str = "overlap", verbose: bool = False,
+                         seed: int = DEFAULT_SEED, pi=None) -> dict:
+    """PermutationProcedure (src/permutations.cpp:160-409).
+
+    Returns ``{"nulls": (M, 7, P), "observed": (M, 7)}`` (plus dimnames).
+    ``seed`` keys the per-permutation shuffle; ``pi`` ((P, n_null) uint32)
+    replaces it with explicit shuffles of the null pool.
+    """
+    return _permutation(discProps, tData, tCorr, tNet, moduleAssignments, modules, nPermutations,
+                        nCores, nullHypothesis, verbose, seed, pi)
+
+
+def PermutationProcedureNoData(discProps: dict, tCorr: RMatrix, tNet: RMatrix, moduleAssignments,
+                               modules, nPermutations: int, nCores: int = 1,
+                               nullHypothesis: str = "overlap", verbose: bool = False,
+                               seed: int = DEFAULT_SEED, pi=None) -> dict:
+    """PermutationProcedureNoData (src/permutationsNoData.cpp:140-375)."""
+    return _permutation(discProps, None, tCorr, tNet, moduleAssignments, modules, nPermutations,
+                        nCores, nullHypothesis, verbose, seed, pi)
+
+
+def _netprops(data, net, module_assignments, modules):
+    lib = L.load()
+    names, labels = _assignments(module_assignments)
+    modules = [str(m) for m in modules]
+    node_names = list(net.colnames)
+    netv = net.f
+    x = data.f if data is not None else None
+    s = x.shape[0] if x is not None else 0
+    k_all = {}
+    for lab in labels:
+        k_all[lab] = k_all.get(lab, 0) + 1
+    tot = sum(k_all.get(m, 0) for m in modules)
+    nm_ = len(modules)
+    deg = np.empty(max(tot, 1))
+    aw = np.empty(max(nm_, 1))
+    kk = np.zeros(max(nm_, 1), dtype=np.int64)
+    nc = np.empty(max(tot, 1)) if x is not None else None
+    sp = np.empty(max(nm_ * s, 1)) if x is not None else None
+    coh = np.empty(max(nm_, 1)) if x is not None else None
+    nn, _k1 = _strv(node_names)
+    an, _k2 = _strv(names)
+    al, _k3 = _strv(labels)
+    mo, _k4 = _strv(modules)
+    L.check_api(lib.netrep_NetProps(_dptr(x), _dptr(netv), s, len(node_names), nn, an, al, len(names),
+                                    mo, nm_, _dptr(deg), _dptr(nc), _dptr(sp), _dptr(coh), _dptr(aw),
+                                    kk.ctypes.data_as(C.POINTER(C.c_int64))))
+    mod_nodes = {}
+    for nm, lab in zip(names, labels):
+        mod_nodes.setdefault(lab, []).append(nm)
+    res = {}
+    o = 0
+    for i, m in enumerate(modules):
+        k = int(kk[i])
+        entry = {"degree": deg[o:o + k].copy(), "avgWeight": float(aw[i]),
+                 "node_names": mod_nodes.get(m, [])}
+        if x is not None:
+            entry.update(summary=sp[i * s:(i + 1) * s].copy(), contribution=nc[o:o + k].copy(),
+                         coherence=float(coh[i]))
+        res[m] = entry
+        o += k
+    return res
+
+
+def NetProps(data: RMatrix, net: RMatrix, moduleAssignments, modules) -> dict:
+    """NetProps (src/properties.cpp:41-156). ``data`` is unscaled; it is scaled on the GPU."""
+    return _netprops(data, net, moduleAssignments, modules)
+
+
+def NetPropsNoData(net: RMatrix, moduleAssignments, modules) -> dict:
+    """NetPropsNoData (src/properties.cpp:190-273)."""
+    return _netprops(None, net, moduleAssignments, modules)

@@ -1,0 +1,816 @@
+// Engine layer of the C ABI (include/netrep_gpu.h): per-GPU context, dataset
+// residency in HBM, batched permutation launches, progress and cancellation.
+//
+// Replaces PermutationProcedure's thread pool (src/permutations.cpp:334-380):
+// instead of nThreads contiguous chunks of permutations walked one module at a
+// time, a launch evaluates every (permutation, module) item of a batch of
+// permutations; batches run back to back on one stream, and the host thread
+// only polls progress / cancellation between batches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/netrep_gpu.h"
+#include "kernels.h"
+#include "prp.h"
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct DeviceTimer {
+  double ms = 0.0;
+  int64_t launches = 0;
+  int64_t items = 0;
+};
+
+}  // namespace
+
+struct nr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::mutex mu;
+
+  // resident dataset
+  double2* d_pairs = nullptr;
+  double* d_data = nullptr;
+  int64_t n_nodes = 0, n_samples = 0;
+  int symmetric = 0;
+
+  // modules
+  int32_t n_rows = 0, n_present = 0, k_max = 0;
+  int64_t n_node_total = 0, n_cv_total = 0;
+  std::vector<int64_t> node_off_h, cv_off_h;
+  int32_t* d_row_of = nullptr;
+  int64_t* d_node_off = nullptr;
+  int64_t* d_cv_off = nullptr;
+  int32_t* d_test_idx = nullptr;
+  int32_t* d_null_pos = nullptr;
+  double* d_disc_cv = nullptr;
+  double* d_disc_wd = nullptr;
+  double* d_disc_nc = nullptr;
+  double* d_cv_shift = nullptr;
+  int32_t* d_mod_order = nullptr;
+
+  // null pool
+  int32_t* d_null_idx = nullptr;
+  int64_t n_null = 0;
+
+  // run buffers
+  double* d_out = nullptr;
+  size_t out_cap = 0;
+  double* h_stage = nullptr;
+  size_t stage_cap = 0;
+  uint32_t* d_pi = nullptr;
+  size_t pi_cap = 0;
+  double* d_scratch = nullptr;
+  size_t scratch_cap = 0;
+  int* d_counters = nullptr;  // [0] queue head, [1] lanczos cap hits, [2] flag
+  int64_t batch = 0;          // 0 = automatic
+
+  std::atomic<int64_t> done{0}, total{0};
+  std::atomic<bool> cancel{false};
+
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  DeviceTimer timers[2];
+};
+
+namespace {
+
+int fail(nr_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int hip_fail(nr_ctx* ctx, hipError_t e, const char* what) {
+  return fail(ctx, e == hipErrorOutOfMemory ? NR_ERR_OOM : NR_ERR_HIP,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define NR_HIP(ctx, call)                              \
+  do {                                                 \
+    hipError_t e_ = (call);                            \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+  } while (0)
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+template <typename T>
+int upload(nr_ctx* ctx, T*& dst, const T* src, size_t n) {
+  dfree(dst);
+  if (n == 0 || src == nullptr) return NR_OK;
+  NR_HIP(ctx, hipMalloc((void**)&dst, n * sizeof(T)));
+  NR_HIP(ctx, hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  return NR_OK;
+}
+
+template <typename T>
+int ensure(nr_ctx* ctx, T*& buf, size_t& cap, size_t n) {
+  if (n <= cap && buf) return NR_OK;
+  dfree(buf);
+  NR_HIP(ctx, hipMalloc((void**)&buf, n * sizeof(T)));
+  cap = n;
+  return NR_OK;
+}
+
+int ensure_stage(nr_ctx* ctx, size_t n) {
+  if (n <= ctx->stage_cap && ctx->h_stage) return NR_OK;
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  ctx->h_stage = nullptr;
+  NR_HIP(ctx, hipHostMalloc((void**)&ctx->h_stage, n * sizeof(double), hipHostMallocDefault));
+  ctx->stage_cap = n;
+  return NR_OK;
+}
+
+__global__ void na_fill_kernel(double* p, int64_t n) {
+  const double na = __longlong_as_double(0x7FF00000000007A2ll);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = na;
+}
+
+int fill_na(nr_ctx* ctx, double* d, int64_t n) {
+  if (n <= 0) return NR_OK;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(na_fill_kernel, dim3(g), dim3(256), 0, ctx->stream, d, n);
+  NR_HIP(ctx, hipGetLastError());
+  return NR_OK;
+}
+
+int n_stat_of(const nr_ctx* ctx) { return ctx->d_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA; }
+
+int profile_slots(const nr_ctx* ctx, int64_t n_items) {
+  int dev_cu = 256;
+  (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+  const int64_t slots = std::min<int64_t>(n_items, (int64_t)dev_cu * 2);
+  return (int)std::max<int64_t>(slots, 1);
+}
+
+int profile_m_max(int k_max) { return std::min(k_max, 512); }
+int round16(int k) { return (k + 15) / 16 * 16; }
+
+int ensure_scratch(nr_ctx* ctx, int slots, int k_max, int64_t* stride_out) {
+  const int kp = round16(k_max);
+  const int64_t stride = (int64_t)kp * kp + (int64_t)k_max * profile_m_max(k_max);
+  *stride_out = stride;
+  return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(stride * slots));
+}
+
+void timer_begin(nr_ctx* ctx, int which) {
+  if (ctx->timing) (void)hipEventRecord(ctx->ev[2 * which], ctx->stream);
+}
+
+void timer_end(nr_ctx* ctx, int which, int64_t items) {
+  if (!ctx->timing) return;
+  (void)hipEventRecord(ctx->ev[2 * which + 1], ctx->stream);
+  (void)hipEventSynchronize(ctx->ev[2 * which + 1]);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, ctx->ev[2 * which], ctx->ev[2 * which + 1]);
+  ctx->timers[which].ms += ms;
+  ctx->timers[which].launches += 1;
+  ctx->timers[which].items += items;
+}
+
+nr::IndexSource make_source(const nr_ctx* ctx, int mode, uint64_t seed, int64_t perm_base,
+                            const uint32_t* d_pi, const int32_t* direct) {
+  nr::IndexSource s;
+  s.mode = mode;
+  s.seed = seed;
+  s.perm_base = perm_base;
+  s.n_null = (uint32_t)ctx->n_null;
+  s.null_idx = ctx->d_null_idx;
+  s.null_pos = ctx->d_null_pos;
+  s.pi = d_pi;
+  s.direct_idx = direct;
+  return s;
+}
+
+// Launch the statistics kernels for n_perm permutations (or the observed /
+// direct sets when src.mode == NR_IDX_DIRECT, n_perm == 1) into d_out.
+int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double* d_out) {
+  const int n_stat = n_stat_of(ctx);
+  const bool data = ctx->d_data != nullptr;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  int rc = fill_na(ctx, d_out, (int64_t)ctx->n_rows * n_stat * n_perm);
+  if (rc) return rc;
+  if (ctx->n_present == 0) return NR_OK;
+  const int64_t n_items = (int64_t)ctx->n_present * n_perm;
+
+  nr::NetParams np{};
+  np.pairs = ctx->d_pairs;
+  np.n_nodes = ctx->n_nodes;
+  np.symmetric = ctx->symmetric;
+  np.src = src;
+  np.node_off = ctx->d_node_off;
+  np.cv_off = ctx->d_cv_off;
+  np.disc_cv = ctx->d_disc_cv;
+  np.disc_wd = ctx->d_disc_wd;
+  np.cv_shift = ctx->d_cv_shift;
+  np.mod_order = ctx->d_mod_order;
+  np.n_perm = (int32_t)n_perm;
+  np.k_max = ctx->k_max;
+  np.row_of = ctx->d_row_of;
+  np.n_rows = ctx->n_rows;
+  np.n_stat = n_stat;
+  // slots: data path src/permutations.cpp:95-101; network-only src/permutationsNoData.cpp:82-85
+  np.slot_avg_weight = 0;
+  np.slot_cor_cor = data ? 2 : 1;
+  np.slot_cor_degree = data ? 3 : 2;
+  np.slot_avg_cor = data ? 5 : 3;
+  np.out = d_out;
+  timer_begin(ctx, 0);
+  NR_HIP(ctx, nr::launch_net(np, n_items, ctx->stream));
+  timer_end(ctx, 0, n_items);
+
+  if (data) {
+    const int slots = profile_slots(ctx, n_items);
+    int64_t stride = 0;
+    rc = ensure_scratch(ctx, slots, ctx->k_max, &stride);
+    if (rc) return rc;
+    NR_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream));
+    nr::ProfileParams pp{};
+    pp.data = ctx->d_data;
+    pp.n_samples = ctx->n_samples;
+    pp.src = src;
+    pp.node_off = ctx->d_node_off;
+    pp.disc_nc = ctx->d_disc_nc;
+    pp.mod_order = ctx->d_mod_order;
+    pp.n_perm = (int32_t)n_perm;
+    pp.n_items = (int32_t)n_items;
+    pp.k_max = ctx->k_max;
+    pp.kp = round16(ctx->k_max);
+    pp.m_max = profile_m_max(ctx->k_max);
+    pp.row_of = ctx->d_row_of;
+    pp.n_rows = ctx->n_rows;
+    pp.n_stat = n_stat;
+    pp.slot_coherence = 1;
+    pp.slot_cor_contrib = 4;
+    pp.slot_avg_contrib = 6;
+    pp.out = d_out;
+    pp.scratch = ctx->d_scratch;
+    pp.scratch_stride = stride;
+    pp.queue = ctx->d_counters;
+    pp.diag = ctx->d_counters + 1;
+    timer_begin(ctx, 1);
+    NR_HIP(ctx, nr::launch_profile(pp, slots, ctx->stream));
+    timer_end(ctx, 1, n_items);
+  }
+  return NR_OK;
+}
+
+int64_t auto_batch(const nr_ctx* ctx) {
+  if (ctx->batch > 0) return ctx->batch;
+  // Enough items to fill 256 CUs many times over; the profile path keeps the
+  // batch small so per-slot scratch stays hot in the Infinity Cache.
+  const int64_t items_target = ctx->d_data ? 4096 : 65536;
+  return std::max<int64_t>(1, items_target / std::max<int32_t>(ctx->n_present, 1));
+}
+
+int check_ready(nr_ctx* ctx, bool need_null) {
+  if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset: call nr_set_dataset first");
+  if (ctx->n_rows <= 0) return fail(ctx, NR_ERR_INVALID, "no modules: call nr_set_modules first");
+  if (need_null && ctx->n_present > 0 && (!ctx->d_null_idx || !ctx->d_null_pos))
+    return fail(ctx, NR_ERR_INVALID, "no null pool: call nr_set_null_pool and pass null_pos");
+  return NR_OK;
+}
+
+int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* pi, bool pi_on_device,
+             double* nulls, bool nulls_on_device) {
+  int rc = check_ready(ctx, true);
+  if (rc) return rc;
+  if (e < b) return fail(ctx, NR_ERR_INVALID, "perm_end < perm_begin");
+  const int n_stat = n_stat_of(ctx);
+  const int64_t slice = (int64_t)ctx->n_rows * n_stat;
+  const int64_t batch = auto_batch(ctx);
+  ctx->done = 0;
+  ctx->total = e - b;
+  ctx->cancel = false;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  for (int64_t p0 = b; p0 < e; p0 += batch) {
+    if (ctx->cancel.load()) return fail(ctx, NR_ERR_CANCELLED, "permutation procedure cancelled");
+    const int64_t np = std::min(batch, e - p0);
+    const uint32_t* d_pi = nullptr;
+    if (pi) {
+      if (pi_on_device) {
+        d_pi = pi + (p0 - b) * ctx->n_null;
+      } else {
+        rc = ensure(ctx, ctx->d_pi, ctx->pi_cap, (size_t)(np * ctx->n_null));
+        if (rc) return rc;
+        NR_HIP(ctx, hipMemcpyAsync(ctx->d_pi, pi + (p0 - b) * ctx->n_null,
+                                   (size_t)(np * ctx->n_null) * sizeof(uint32_t),
+                                   hipMemcpyHostToDevice, ctx->stream));
+        d_pi = ctx->d_pi;
+      }
+    }
+    const nr::IndexSource src =
+        make_source(ctx, pi ? nr::NR_IDX_TABLE : nr::NR_IDX_PRP, seed, p0, d_pi, nullptr);
+    double* d_out;
+    if (nulls_on_device) {
+      d_out = nulls + (p0 - b) * slice;
+    } else {
+      rc = ensure(ctx, ctx->d_out, ctx->out_cap, (size_t)(np * slice));
+      if (rc) return rc;
+      d_out = ctx->d_out;
+    }
+    rc = launch_batch(ctx, src, np, d_out);
+    if (rc) return rc;
+    if (!nulls_on_device) {
+      rc = ensure_stage(ctx, (size_t)(np * slice));
+      if (rc) return rc;
+      NR_HIP(ctx, hipMemcpyAsync(ctx->h_stage, d_out, (size_t)(np * slice) * sizeof(double),
+                                 hipMemcpyDeviceToHost, ctx->stream));
+      NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      std::memcpy(nulls + (p0 - b) * slice, ctx->h_stage, (size_t)(np * slice) * sizeof(double));
+    } else {
+      NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    ctx->done += np;
+  }
+  return NR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nr_device_count(int* count) {
+  if (!count) return NR_ERR_INVALID;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return NR_OK;
+}
+
+int nr_ctx_create(int device, nr_ctx** out) {
+  if (!out) return NR_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    g_create_error = "no HIP device available (the MI355X engine has no CPU fallback)";
+    return NR_ERR_HIP;
+  }
+  if (device < 0 || device >= n) {
+    g_create_error = "device index out of range";
+    return NR_ERR_INVALID;
+  }
+  nr_ctx* ctx = new nr_ctx();
+  ctx->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
+  if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, 16 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, 16 * sizeof(int));
+  if (e != hipSuccess) {
+    g_create_error = std::string("context creation failed: ") + hipGetErrorString(e);
+    nr_ctx_destroy(ctx);
+    return NR_ERR_HIP;
+  }
+  *out = ctx;
+  return NR_OK;
+}
+
+void nr_ctx_destroy(nr_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  dfree(ctx->d_pairs);
+  dfree(ctx->d_data);
+  dfree(ctx->d_row_of);
+  dfree(ctx->d_node_off);
+  dfree(ctx->d_cv_off);
+  dfree(ctx->d_test_idx);
+  dfree(ctx->d_null_pos);
+  dfree(ctx->d_disc_cv);
+  dfree(ctx->d_disc_wd);
+  dfree(ctx->d_disc_nc);
+  dfree(ctx->d_cv_shift);
+  dfree(ctx->d_mod_order);
+  dfree(ctx->d_null_idx);
+  dfree(ctx->d_out);
+  dfree(ctx->d_pi);
+  dfree(ctx->d_scratch);
+  dfree(ctx->d_counters);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  for (auto& ev : ctx->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* nr_last_error(const nr_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const double* data,
+                   int64_t n_nodes, int64_t n_samples, int where) {
+  if (!ctx) return NR_ERR_INVALID;
+  if (!corr || !net || n_nodes <= 0) return fail(ctx, NR_ERR_INVALID, "corr/net missing or n_nodes <= 0");
+  if (data && n_samples < 2) return fail(ctx, NR_ERR_INVALID, "data needs n_samples >= 2");
+  if (n_nodes > (int64_t)INT32_MAX) return fail(ctx, NR_ERR_UNSUPPORTED, "n_nodes exceeds 2^31-1");
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  dfree(ctx->d_pairs);
+  dfree(ctx->d_data);
+  ctx->n_nodes = n_nodes;
+  ctx->n_samples = data ? n_samples : 0;
+  const int64_t n_elem = n_nodes * n_nodes;
+  NR_HIP(ctx, hipMalloc((void**)&ctx->d_pairs, (size_t)n_elem * sizeof(double2)));
+  if (where == NR_DEVICE) {
+    NR_HIP(ctx, nr::launch_interleave(corr, net, ctx->d_pairs, n_elem, ctx->stream));
+  } else {
+    // Stream the host matrices through two staging buffers in chunks.
+    const int64_t chunk = std::min<int64_t>(n_elem, (int64_t)1 << 25);  // 256 MiB per matrix
+    double *tc = nullptr, *tn = nullptr;
+    NR_HIP(ctx, hipMalloc((void**)&tc, (size_t)chunk * sizeof(double)));
+    hipError_t e = hipMalloc((void**)&tn, (size_t)chunk * sizeof(double));
+    if (e != hipSuccess) {
+      (void)hipFree(tc);
+      return hip_fail(ctx, e, "hipMalloc staging");
+    }
+    for (int64_t o = 0; o < n_elem && e == hipSuccess; o += chunk) {
+      const int64_t len = std::min(chunk, n_elem - o);
+      e = hipMemcpyAsync(tc, corr + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(tn, net + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
+      if (e == hipSuccess) e = nr::launch_interleave(tc, tn, ctx->d_pairs + o, len, ctx->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    }
+    (void)hipFree(tc);
+    (void)hipFree(tn);
+    if (e != hipSuccess) return hip_fail(ctx, e, "dataset upload");
+  }
+  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 2, 0, sizeof(int), ctx->stream));
+  NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 2, ctx->stream));
+  int asym = 0;
+  NR_HIP(ctx, hipMemcpyAsync(&asym, ctx->d_counters + 2, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  if (data) {
+    const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
+    NR_HIP(ctx, hipMalloc((void**)&ctx->d_data, bytes));
+    NR_HIP(ctx, hipMemcpyAsync(ctx->d_data, data, bytes,
+                               where == NR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                               ctx->stream));
+  }
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->symmetric = asym ? 0 : 1;
+  return NR_OK;
+}
+
+int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric) {
+  if (!ctx || !symmetric) return NR_ERR_INVALID;
+  if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset");
+  *symmetric = ctx->symmetric;
+  return NR_OK;
+}
+
+int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t* row_of,
+                   const int64_t* node_off, const int32_t* test_idx, const int32_t* null_pos,
+                   const double* disc_corr, const double* disc_degree, const double* disc_contrib) {
+  if (!ctx) return NR_ERR_INVALID;
+  if (n_rows < 0 || n_present < 0 || n_present > n_rows)
+    return fail(ctx, NR_ERR_INVALID, "bad n_rows / n_present");
+  if (n_present > 0 && (!row_of || !node_off || !test_idx || !disc_corr || !disc_degree))
+    return fail(ctx, NR_ERR_INVALID, "module arrays missing");
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->n_rows = n_rows;
+  ctx->n_present = n_present;
+  ctx->node_off_h.assign(node_off, node_off + (n_present > 0 ? n_present + 1 : 0));
+  if (n_present == 0) ctx->node_off_h.assign(1, 0);
+  ctx->cv_off_h.assign(n_present + 1, 0);
+  int32_t kmax = 0;
+  std::vector<double> shift(n_present, 0.0);
+  for (int m = 0; m < n_present; ++m) {
+    const int64_t k = node_off[m + 1] - node_off[m];
+    if (k <= 0) return fail(ctx, NR_ERR_INVALID, "present module with no nodes");
+    if (k > NR_MAX_MODULE_NODES)
+      return fail(ctx, NR_ERR_UNSUPPORTED, "module larger than NR_MAX_MODULE_NODES nodes");
+    if (row_of[m] < 0 || row_of[m] >= n_rows) return fail(ctx, NR_ERR_INVALID, "row_of out of range");
+    kmax = std::max<int32_t>(kmax, (int32_t)k);
+    ctx->cv_off_h[m + 1] = ctx->cv_off_h[m] + k * (k - 1) / 2;
+    for (int64_t v = 0; v < k * (k - 1) / 2; ++v) {
+      const double x = disc_corr[ctx->cv_off_h[m] + v];
+      if (std::isfinite(x)) {
+        shift[m] = x;
+        break;
+      }
+    }
+  }
+  ctx->k_max = kmax;
+  ctx->n_node_total = ctx->node_off_h.back();
+  ctx->n_cv_total = ctx->cv_off_h.back();
+  for (int64_t i = 0; i < ctx->n_node_total; ++i)
+    if (test_idx[i] < 0 || test_idx[i] >= ctx->n_nodes)
+      return fail(ctx, NR_ERR_INVALID, "test_idx outside the resident dataset (call nr_set_dataset first)");
+  std::vector<int32_t> order(n_present);
+  for (int m = 0; m < n_present; ++m) order[m] = m;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return (node_off[a + 1] - node_off[a]) > (node_off[b + 1] - node_off[b]);
+  });
+  int rc;
+  if ((rc = upload(ctx, ctx->d_row_of, row_of, n_present))) return rc;
+  if ((rc = upload(ctx, ctx->d_node_off, ctx->node_off_h.data(), ctx->node_off_h.size()))) return rc;
+  if ((rc = upload(ctx, ctx->d_cv_off, ctx->cv_off_h.data(), ctx->cv_off_h.size()))) return rc;
+  if ((rc = upload(ctx, ctx->d_test_idx, test_idx, (size_t)ctx->n_node_total))) return rc;
+  if ((rc = upload(ctx, ctx->d_null_pos, null_pos, null_pos ? (size_t)ctx->n_node_total : 0))) return rc;
+  if ((rc = upload(ctx, ctx->d_disc_cv, disc_corr, (size_t)ctx->n_cv_total))) return rc;
+  if ((rc = upload(ctx, ctx->d_disc_wd, disc_degree, (size_t)ctx->n_node_total))) return rc;
+  if ((rc = upload(ctx, ctx->d_disc_nc, disc_contrib, disc_contrib ? (size_t)ctx->n_node_total : 0))) return rc;
+  if ((rc = upload(ctx, ctx->d_cv_shift, shift.data(), shift.size()))) return rc;
+  if ((rc = upload(ctx, ctx->d_mod_order, order.data(), order.size()))) return rc;
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->d_data && !ctx->d_disc_nc && n_present > 0)
+    return fail(ctx, NR_ERR_INVALID, "dataset has data but disc_contrib is NULL");
+  return NR_OK;
+}
+
+int nr_set_null_pool(nr_ctx* ctx, const int32_t* null_idx, int64_t n_null) {
+  if (!ctx) return NR_ERR_INVALID;
+  if (!null_idx || n_null <= 0 || n_null > (int64_t)UINT32_MAX / 4)
+    return fail(ctx, NR_ERR_INVALID, "bad null pool");
+  for (int64_t i = 0; i < n_null; ++i)
+    if (null_idx[i] < 0 || null_idx[i] >= ctx->n_nodes)
+      return fail(ctx, NR_ERR_INVALID, "null_idx outside the resident dataset");
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->n_null = n_null;
+  int rc = upload(ctx, ctx->d_null_idx, null_idx, (size_t)n_null);
+  if (rc) return rc;
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return NR_OK;
+}
+
+int nr_observed(nr_ctx* ctx, double* observed) {
+  if (!ctx || !observed) return NR_ERR_INVALID;
+  int rc = check_ready(ctx, false);
+  if (rc) return rc;
+  const int64_t slice = (int64_t)ctx->n_rows * n_stat_of(ctx);
+  rc = ensure(ctx, ctx->d_out, ctx->out_cap, (size_t)slice);
+  if (rc) return rc;
+  const nr::IndexSource src = make_source(ctx, nr::NR_IDX_DIRECT, 0, 0, nullptr, ctx->d_test_idx);
+  rc = launch_batch(ctx, src, 1, ctx->d_out);
+  if (rc) return rc;
+  NR_HIP(ctx, hipMemcpyAsync(observed, ctx->d_out, (size_t)slice * sizeof(double),
+                             hipMemcpyDeviceToHost, ctx->stream));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return NR_OK;
+}
+
+int nr_run(nr_ctx* ctx, int64_t perm_begin, int64_t perm_end, uint64_t seed, const uint32_t* pi,
+           double* nulls) {
+  if (!ctx || !nulls) return NR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return run_impl(ctx, perm_begin, perm_end, seed, pi, false, nulls, false);
+}
+
+int nr_run_device(nr_ctx* ctx, int64_t perm_begin, int64_t perm_end, uint64_t seed,
+                  const uint32_t* pi_device, double* nulls_device) {
+  if (!ctx || !nulls_device) return NR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return run_impl(ctx, perm_begin, perm_end, seed, pi_device, true, nulls_device, true);
+}
+
+int nr_export_indices(nr_ctx* ctx, int64_t perm_begin, int64_t perm_end, uint64_t seed,
+                      int32_t* indices) {
+  if (!ctx || !indices || perm_end < perm_begin) return NR_ERR_INVALID;
+  int rc = check_ready(ctx, true);
+  if (rc) return rc;
+  const int64_t np = perm_end - perm_begin;
+  if (np == 0) return NR_OK;
+  int32_t* d = nullptr;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipMalloc((void**)&d, (size_t)(np * ctx->n_node_total) * sizeof(int32_t)));
+  const nr::IndexSource src = make_source(ctx, nr::NR_IDX_PRP, seed, perm_begin, nullptr, nullptr);
+  hipError_t e = nr::launch_export(src, ctx->n_node_total, d, np, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(indices, d, (size_t)(np * ctx->n_node_total) * sizeof(int32_t),
+                       hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "export indices");
+  return NR_OK;
+}
+
+int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const int32_t* idx,
+                      double* corr_vec, double* degree, double* avg_weight, double* contribution,
+                      double* summary, double* coherence) {
+  if (!ctx || n_mod < 0 || (n_mod > 0 && (!node_off || !idx))) return NR_ERR_INVALID;
+  if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset");
+  if ((contribution || summary || coherence) && !ctx->d_data)
+    return fail(ctx, NR_ERR_INVALID, "contribution/summary need a dataset with data");
+  if (n_mod == 0) return NR_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  std::vector<int64_t> cv(n_mod + 1, 0);
+  int32_t kmax = 0;
+  for (int m = 0; m < n_mod; ++m) {
+    const int64_t k = node_off[m + 1] - node_off[m];
+    if (k <= 0) return fail(ctx, NR_ERR_INVALID, "module with no nodes");
+    if (k > NR_MAX_MODULE_NODES) return fail(ctx, NR_ERR_UNSUPPORTED, "module larger than NR_MAX_MODULE_NODES");
+    kmax = std::max<int32_t>(kmax, (int32_t)k);
+    cv[m + 1] = cv[m] + k * (k - 1) / 2;
+  }
+  const int64_t nodes = node_off[n_mod];
+  for (int64_t i = 0; i < nodes; ++i)
+    if (idx[i] < 0 || idx[i] >= ctx->n_nodes) return fail(ctx, NR_ERR_INVALID, "idx outside the dataset");
+  std::vector<int32_t> order(n_mod);
+  for (int m = 0; m < n_mod; ++m) order[m] = m;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return (node_off[a + 1] - node_off[a]) > (node_off[b + 1] - node_off[b]);
+  });
+  int64_t *d_off = nullptr, *d_cv = nullptr;
+  int32_t *d_idx = nullptr, *d_order = nullptr;
+  double *d_cvo = nullptr, *d_wd = nullptr, *d_nc = nullptr, *d_sp = nullptr, *d_coh = nullptr,
+         *d_aw = nullptr;
+  int rc = NR_OK;
+  auto cleanup = [&]() {
+    dfree(d_off); dfree(d_cv); dfree(d_idx); dfree(d_order);
+    dfree(d_cvo); dfree(d_wd); dfree(d_nc); dfree(d_sp); dfree(d_coh); dfree(d_aw);
+  };
+  const int64_t S = ctx->n_samples;
+  do {
+    if ((rc = upload(ctx, d_off, node_off, (size_t)n_mod + 1))) break;
+    if ((rc = upload(ctx, d_cv, cv.data(), cv.size()))) break;
+    if ((rc = upload(ctx, d_idx, idx, (size_t)nodes))) break;
+    if ((rc = upload(ctx, d_order, order.data(), order.size()))) break;
+    hipError_t e = hipMalloc((void**)&d_cvo, (size_t)std::max<int64_t>(cv.back(), 1) * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_wd, (size_t)nodes * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_aw, (size_t)n_mod * sizeof(double));
+    if (e == hipSuccess && ctx->d_data) e = hipMalloc((void**)&d_nc, (size_t)nodes * sizeof(double));
+    if (e == hipSuccess && ctx->d_data) e = hipMalloc((void**)&d_sp, (size_t)(n_mod * S) * sizeof(double));
+    if (e == hipSuccess && ctx->d_data) e = hipMalloc((void**)&d_coh, (size_t)n_mod * sizeof(double));
+    if (e != hipSuccess) { rc = hip_fail(ctx, e, "hipMalloc module vectors"); break; }
+    nr::IndexSource src = make_source(ctx, nr::NR_IDX_DIRECT, 0, 0, nullptr, d_idx);
+    nr::NetParams np{};
+    np.pairs = ctx->d_pairs;
+    np.n_nodes = ctx->n_nodes;
+    np.symmetric = ctx->symmetric;
+    np.src = src;
+    np.node_off = d_off;
+    np.cv_off = d_cv;
+    np.mod_order = d_order;
+    np.n_perm = 1;
+    np.k_max = kmax;
+    np.cv_out = d_cvo;
+    np.wd_out = d_wd;
+    np.avgw_out = d_aw;
+    e = nr::launch_net(np, n_mod, ctx->stream);
+    if (e == hipSuccess && ctx->d_data && (contribution || summary || coherence)) {
+      const int slots = profile_slots(ctx, n_mod);
+      int64_t stride = 0;
+      if ((rc = ensure_scratch(ctx, slots, kmax, &stride))) break;
+      e = hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream);
+      nr::ProfileParams pp{};
+      pp.data = ctx->d_data;
+      pp.n_samples = S;
+      pp.src = src;
+      pp.node_off = d_off;
+      pp.mod_order = d_order;
+      pp.n_perm = 1;
+      pp.n_items = n_mod;
+      pp.k_max = kmax;
+      pp.kp = round16(kmax);
+      pp.m_max = profile_m_max(kmax);
+      pp.sp_out = d_sp;
+      pp.nc_out = d_nc;
+      pp.coh_out = d_coh;
+      pp.scratch = ctx->d_scratch;
+      pp.scratch_stride = stride;
+      pp.queue = ctx->d_counters;
+      pp.diag = ctx->d_counters + 1;
+      if (e == hipSuccess) e = nr::launch_profile(pp, slots, ctx->stream);
+    }
+    auto d2h = [&](double* h, const double* d, int64_t n) {
+      if (e == hipSuccess && h && n > 0)
+        e = hipMemcpyAsync(h, d, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+    };
+    d2h(corr_vec, d_cvo, cv.back());
+    d2h(degree, d_wd, nodes);
+    d2h(avg_weight, d_aw, n_mod);
+    d2h(contribution, d_nc, nodes);
+    d2h(summary, d_sp, n_mod * S);
+    d2h(coherence, d_coh, n_mod);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) rc = hip_fail(ctx, e, "module vectors");
+  } while (0);
+  cleanup();
+  return rc;
+}
+
+int nr_scale(nr_ctx* ctx, const double* data, int64_t n_samples, int64_t n_nodes, double* scaled) {
+  if (!ctx || !data || !scaled || n_samples <= 0 || n_nodes <= 0) return NR_ERR_INVALID;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
+  double *din = nullptr, *dout = nullptr;
+  NR_HIP(ctx, hipMalloc((void**)&din, bytes));
+  hipError_t e = hipMalloc((void**)&dout, bytes);
+  if (e == hipSuccess) e = hipMemcpyAsync(din, data, bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = nr::launch_scale(din, dout, n_samples, n_nodes, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(scaled, dout, bytes, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(din);
+  if (dout) (void)hipFree(dout);
+  if (e != hipSuccess) return hip_fail(ctx, e, "scale");
+  return NR_OK;
+}
+
+int nr_check_finite(nr_ctx* ctx, const double* mat, int64_t n_elem, int* all_finite) {
+  if (!ctx || !mat || !all_finite || n_elem < 0) return NR_ERR_INVALID;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  *all_finite = 1;
+  if (n_elem == 0) return NR_OK;
+  const int64_t chunk = std::min<int64_t>(n_elem, (int64_t)1 << 26);
+  double* d = nullptr;
+  NR_HIP(ctx, hipMalloc((void**)&d, (size_t)chunk * sizeof(double)));
+  hipError_t e = hipMemsetAsync(ctx->d_counters + 2, 0, sizeof(int), ctx->stream);
+  for (int64_t o = 0; o < n_elem && e == hipSuccess; o += chunk) {
+    const int64_t len = std::min(chunk, n_elem - o);
+    e = hipMemcpyAsync(d, mat + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = nr::launch_finite(d, len, ctx->d_counters + 2, ctx->stream);
+  }
+  int bad = 0;
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(&bad, ctx->d_counters + 2, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(ctx, e, "check finite");
+  *all_finite = bad ? 0 : 1;
+  return NR_OK;
+}
+
+int nr_progress(nr_ctx* ctx, int64_t* done, int64_t* total) {
+  if (!ctx) return NR_ERR_INVALID;
+  if (done) *done = ctx->done.load();
+  if (total) *total = ctx->total.load();
+  return NR_OK;
+}
+
+int nr_cancel(nr_ctx* ctx) {
+  if (!ctx) return NR_ERR_INVALID;
+  ctx->cancel = true;
+  return NR_OK;
+}
+
+int nr_set_batch(nr_ctx* ctx, int64_t perms_per_launch) {
+  if (!ctx || perms_per_launch < 0) return NR_ERR_INVALID;
+  ctx->batch = perms_per_launch;
+  return NR_OK;
+}
+
+int nr_set_timing(nr_ctx* ctx, int enable) {
+  if (!ctx) return NR_ERR_INVALID;
+  ctx->timing = enable != 0;
+  return NR_OK;
+}
+
+int nr_get_timing(nr_ctx* ctx, int kernel, double* total_ms, int64_t* launches, int64_t* items) {
+  if (!ctx || kernel < 0 || kernel > 1) return NR_ERR_INVALID;
+  if (total_ms) *total_ms = ctx->timers[kernel].ms;
+  if (launches) *launches = ctx->timers[kernel].launches;
+  if (items) *items = ctx->timers[kernel].items;
+  return NR_OK;
+}
+
+int nr_reset_timing(nr_ctx* ctx) {
+  if (!ctx) return NR_ERR_INVALID;
+  ctx->timers[0] = DeviceTimer();
+  ctx->timers[1] = DeviceTimer();
+  return NR_OK;
+}
+
+int nr_synchronize(nr_ctx* ctx) {
+  if (!ctx) return NR_ERR_INVALID;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return NR_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+// Host evaluation of the keyed null-pool permutation (prp.h) for tests and
+// for callers that want to export the exact shuffles a run uses.
+int nr_prp_table(uint64_t seed, int64_t perm_begin, int64_t perm_end, int64_t n_null,
+                 uint32_t* out) {
+  if (!out || perm_end < perm_begin || n_null <= 0 || n_null > (int64_t)UINT32_MAX / 4)
+    return NR_ERR_INVALID;
+  for (int64_t p = perm_begin; p < perm_end; ++p) {
+    const nr_prp_key key = nr_prp_make_key(seed, (uint64_t)p, (uint32_t)n_null);
+    for (int64_t q = 0; q < n_null; ++q)
+      out[(p - perm_begin) * n_null + q] = nr_prp_permute(key, (uint32_t)q);
+  }
+  return NR_OK;
+}
+}  // extern "C"

@@ -1,0 +1,439 @@
+// Reference-interface layer of the C ABI (netrep_* in include/netrep_gpu.h).
+//
+// Mirrors NetRep's eight Rcpp entry points (src/RcppExports.cpp:131-146):
+// name maps and index derivation are restated from src/utils.cpp, the driver
+// logic from src/permutations.cpp, src/permutationsNoData.cpp,
+// src/discProps.cpp, src/properties.cpp, src/scale.cpp and
+// src/checkFinite.cpp. All arithmetic on matrices runs on the GPU through the
+// engine layer; this file only resolves names to index sets, moves buffers and
+// shards permutations over GPUs (one host thread + context per GPU, replacing
+// the std::thread pool of src/permutations.cpp:334-380).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/netrep_gpu.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int ctx_err(int code, nr_ctx* ctx) {
+  g_err = nr_last_error(ctx);
+  return code;
+}
+
+typedef std::unordered_map<std::string, int64_t> NameMap;
+
+// MakeIdxMap (src/utils.cpp:5-11).
+NameMap make_idx_map(const char* const* names, int64_t n) {
+  NameMap m;
+  m.reserve((size_t)n * 2);
+  for (int64_t i = 0; i < n; ++i) m[names[i]] = i;
+  return m;
+}
+
+// MakeModMap (src/utils.cpp:21-65): label -> node names. Node order inside a
+// module is the order of appearance in moduleAssignments (the reference's
+// Boost multimap order is implementation-defined; see oracle/netrep_oracle.py).
+struct ModMap {
+  std::unordered_map<std::string, std::vector<std::string>> nodes;
+  const std::vector<std::string>* find(const std::string& label) const {
+    auto it = nodes.find(label);
+    return it == nodes.end() ? nullptr : &it->second;
+  }
+};
+
+ModMap make_mod_map(const char* const* ma_names, const char* const* ma_labels, int64_t n,
+                    const NameMap* present_in) {
+  ModMap mm;
+  for (int64_t i = 0; i < n; ++i) {
+    if (present_in && present_in->find(ma_names[i]) == present_in->end()) continue;
+    mm.nodes[ma_labels[i]].push_back(ma_names[i]);
+  }
+  return mm;
+}
+
+struct CtxDeleter {
+  void operator()(nr_ctx* c) const { nr_ctx_destroy(c); }
+};
+typedef std::unique_ptr<nr_ctx, CtxDeleter> CtxPtr;
+
+int open_ctx(int device, CtxPtr& out) {
+  nr_ctx* c = nullptr;
+  const int rc = nr_ctx_create(device, &c);
+  if (rc) return set_err(rc, nr_last_error(nullptr));
+  out.reset(c);
+  return NR_OK;
+}
+
+int gpu_count_requested() {
+  int avail = 0;
+  nr_device_count(&avail);
+  int want = 1;
+  if (const char* e = std::getenv("NETREP_NUM_GPUS")) want = std::max(1, std::atoi(e));
+  return std::max(1, std::min(want, avail));
+}
+
+// Index sets of the modules present in the test dataset (a4 of SURVEY.md 8).
+struct ModuleSets {
+  int32_t n_rows = 0, n_present = 0;
+  std::vector<int32_t> row_of;
+  std::vector<int64_t> node_off{0};
+  std::vector<int32_t> test_idx, null_pos;
+  std::vector<int32_t> null_idx;
+  std::vector<double> disc_cv, disc_wd, disc_nc;
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* netrep_last_error(void) { return g_err.c_str(); }
+
+int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_data,
+                                const double* t_corr, const double* t_net, int64_t n_samples,
+                                int64_t n_nodes, const char* const* t_names,
+                                const char* const* ma_names, const char* const* ma_labels,
+                                int64_t n_assign, const char* const* modules, int64_t n_modules,
+                                int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
+                                int32_t verbose, uint64_t seed, const uint32_t* pi,
+                                double* nulls_out, double* observed_out) {
+  (void)n_cores;
+  if (!disc || !t_corr || !t_net || !t_names || !ma_names || !ma_labels || !modules ||
+      !observed_out || n_perm < 0 || (n_perm > 0 && !nulls_out) || n_nodes <= 0)
+    return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedure");
+  const bool with_data = t_data != nullptr;
+  if (with_data && !disc->contribution)
+    return set_err(NR_ERR_INVALID, "discProps has no 'contribution' but tData was given");
+  const std::string null_type = null_hypothesis ? null_hypothesis : "overlap";
+  if (null_type != "overlap" && null_type != "all")
+    return set_err(NR_ERR_INVALID, "nullHypothesis must be \"overlap\" or \"all\"");
+
+  // src/permutations.cpp:184-201
+  const NameMap t_idx_map = make_idx_map(t_names, n_nodes);
+  const ModMap present = make_mod_map(ma_names, ma_labels, n_assign, &t_idx_map);
+
+  // MakeNullMap (src/utils.cpp:108-136) over validNodes (src/permutations.cpp:319-323)
+  ModuleSets ms;
+  NameMap null_map;
+  {
+    const char* const* valid = null_type == "overlap" ? ma_names : t_names;
+    const int64_t n_valid = null_type == "overlap" ? n_assign : n_nodes;
+    for (int64_t i = 0; i < n_valid; ++i) {
+      auto it = t_idx_map.find(valid[i]);
+      if (it == t_idx_map.end()) continue;
+      null_map[valid[i]] = (int64_t)ms.null_idx.size();
+      ms.null_idx.push_back((int32_t)it->second);
+    }
+  }
+
+  ms.n_rows = (int32_t)n_modules;
+  for (int64_t mi = 0; mi < n_modules; ++mi) {
+    const std::vector<std::string>* nodes = present.find(modules[mi]);
+    if (!nodes || nodes->empty()) continue;  // modsPresent (src/permutations.cpp:196-201)
+    const int64_t k = (int64_t)nodes->size();
+    if (disc->degree[mi] == nullptr || disc->degree_len[mi] != k || disc->corr[mi] == nullptr ||
+        disc->corr_len[mi] != k * (k - 1) / 2 ||
+        (with_data && (disc->contribution[mi] == nullptr || disc->contribution_len[mi] != k)))
+      return set_err(NR_ERR_INVALID, std::string("discProps vectors of module '") + modules[mi] +
+                                         "' do not match its nodes present in the test dataset");
+    ms.row_of.push_back((int32_t)mi);
+    for (const std::string& nm : *nodes) {
+      ms.test_idx.push_back((int32_t)t_idx_map.at(nm));      // GetNodeIdx src/utils.cpp:147-162
+      auto np = null_map.find(nm);
+      if (np == null_map.end())
+        return set_err(NR_ERR_INVALID, "module node '" + nm + "' is not in the null pool");
+      ms.null_pos.push_back((int32_t)np->second);
+    }
+    ms.node_off.push_back((int64_t)ms.test_idx.size());
+    ms.disc_cv.insert(ms.disc_cv.end(), disc->corr[mi], disc->corr[mi] + k * (k - 1) / 2);
+    ms.disc_wd.insert(ms.disc_wd.end(), disc->degree[mi], disc->degree[mi] + k);
+    if (with_data) ms.disc_nc.insert(ms.disc_nc.end(), disc->contribution[mi], disc->contribution[mi] + k);
+  }
+  ms.n_present = (int32_t)ms.row_of.size();
+  const int n_stat = with_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA;
+
+  const int n_gpu = (n_perm > 0) ? (int)std::min<int64_t>(gpu_count_requested(), std::max<int64_t>(n_perm, 1)) : 1;
+  std::vector<CtxPtr> ctxs(n_gpu);
+  for (int g = 0; g < n_gpu; ++g) {
+    int rc = open_ctx(g, ctxs[g]);
+    if (rc) return rc;
+  }
+  // Each GPU holds its own copy of the test dataset (the multi-rank driver in
+  // bench.py broadcasts it over RCCL instead).
+  std::vector<int> rcs(n_gpu, NR_OK);
+  auto setup = [&](int g) {
+    nr_ctx* c = ctxs[g].get();
+    int rc = nr_set_dataset(c, t_corr, t_net, t_data, n_nodes, n_samples, NR_HOST);
+    if (!rc)
+      rc = nr_set_modules(c, ms.n_rows, ms.n_present, ms.row_of.data(), ms.node_off.data(),
+                          ms.test_idx.data(), ms.null_pos.data(), ms.disc_cv.data(),
+                          ms.disc_wd.data(), with_data ? ms.disc_nc.data() : nullptr);
+    if (!rc && !ms.null_idx.empty()) rc = nr_set_null_pool(c, ms.null_idx.data(), (int64_t)ms.null_idx.size());
+    rcs[g] = rc;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int g = 0; g < n_gpu; ++g) th.emplace_back(setup, g);
+    for (auto& t : th) t.join();
+  }
+  for (int g = 0; g < n_gpu; ++g)
+    if (rcs[g]) return ctx_err(rcs[g], ctxs[g].get());
+
+  // Observed statistics (src/permutations.cpp:246-285).
+  {
+    const int rc = nr_observed(ctxs[0].get(), observed_out);
+    if (rc) return ctx_err(rc, ctxs[0].get());
+  }
+  if (n_perm == 0) return NR_OK;  // src/permutations.cpp:288-299
+
+  // Contiguous permutation chunks, remainder to the first devices
+  // (src/permutations.cpp:338-354).
+  std::vector<int64_t> start(n_gpu + 1, 0);
+  for (int g = 0; g < n_gpu; ++g)
+    start[g + 1] = start[g] + n_perm / n_gpu + (g < n_perm % n_gpu ? 1 : 0);
+  const int64_t slice = (int64_t)ms.n_rows * n_stat;
+  const int64_t n_null = (int64_t)ms.null_idx.size();
+  if (verbose) {
+    std::printf("\n");
+    std::fflush(stdout);
+  }
+  std::vector<std::thread> th;
+  for (int g = 0; g < n_gpu; ++g) {
+    th.emplace_back([&, g]() {
+      rcs[g] = nr_run(ctxs[g].get(), start[g], start[g + 1], seed,
+                      pi ? pi + start[g] * n_null : nullptr, nulls_out + start[g] * slice);
+    });
+  }
+  // Progress monitor (MonitorProgress, src/thread-utils.cpp:49-82).
+  if (verbose) {
+    for (;;) {
+      int64_t done = 0;
+      for (int g = 0; g < n_gpu; ++g) {
+        int64_t d = 0;
+        nr_progress(ctxs[g].get(), &d, nullptr);
+        done += d;
+      }
+      const unsigned pct = (unsigned)std::lround((double)done / (double)n_perm * 100.0);
+      std::printf("\r%5u%% completed.", pct);
+      std::fflush(stdout);
+      if (done >= n_perm) break;
+      bool any_failed = false;
+      for (int g = 0; g < n_gpu; ++g) any_failed |= rcs[g] != NR_OK;
+      if (any_failed) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(200));
+    }
+    std::printf("\n\n");
+    std::fflush(stdout);
+  }
+  for (auto& t : th) t.join();
+  for (int g = 0; g < n_gpu; ++g)
+    if (rcs[g]) return ctx_err(rcs[g], ctxs[g].get());
+  return NR_OK;
+}
+
+int netrep_IntermediateProperties(const double* d_data, const double* d_corr, const double* d_net,
+                                  int64_t n_samples, int64_t n_nodes, const char* const* d_names,
+                                  const char* const* t_node_names, int64_t n_t_nodes,
+                                  const char* const* ma_names, const char* const* ma_labels,
+                                  int64_t n_assign, const char* const* modules, int64_t n_modules,
+                                  double* degree_out, int64_t* degree_len, double* corr_out,
+                                  int64_t* corr_len, double* contribution_out,
+                                  int64_t* contribution_len) {
+  if (!d_corr || !d_net || !d_names || !t_node_names || !ma_names || !ma_labels || !modules ||
+      !degree_out || !degree_len || !corr_out || !corr_len || n_nodes <= 0)
+    return set_err(NR_ERR_INVALID, "invalid arguments to IntermediateProperties");
+  const bool with_data = d_data != nullptr;
+  if (with_data && (!contribution_out || !contribution_len))
+    return set_err(NR_ERR_INVALID, "contribution buffers required with data");
+  // src/discProps.cpp:64-79
+  const NameMap d_idx_map = make_idx_map(d_names, n_nodes);
+  const NameMap t_idx_map = make_idx_map(t_node_names, n_t_nodes);
+  const ModMap present = make_mod_map(ma_names, ma_labels, n_assign, &t_idx_map);
+  std::vector<int64_t> node_off{0};
+  std::vector<int32_t> idx;
+  std::vector<int64_t> which;
+  for (int64_t mi = 0; mi < n_modules; ++mi) {
+    degree_len[mi] = corr_len[mi] = 0;
+    if (with_data) contribution_len[mi] = 0;
+    const std::vector<std::string>* nodes = present.find(modules[mi]);
+    if (!nodes || nodes->empty()) continue;
+    for (const std::string& nm : *nodes) {
+      auto it = d_idx_map.find(nm);  // GetNodeIdx (src/utils.cpp:157) throws on a miss
+      if (it == d_idx_map.end())
+        return set_err(NR_ERR_INVALID, "node '" + nm + "' of moduleAssignments is not in the discovery dataset");
+      idx.push_back((int32_t)it->second);
+    }
+    node_off.push_back((int64_t)idx.size());
+    which.push_back(mi);
+  }
+  const int32_t n_mod = (int32_t)which.size();
+  if (n_mod == 0) return NR_OK;
+  CtxPtr ctx;
+  int rc = open_ctx(0, ctx);
+  if (rc) return rc;
+  rc = nr_set_dataset(ctx.get(), d_corr, d_net, d_data, n_nodes, n_samples, NR_HOST);
+  if (rc) return ctx_err(rc, ctx.get());
+  const int64_t nodes = node_off.back();
+  int64_t n_cv = 0;
+  for (int32_t m = 0; m < n_mod; ++m) {
+    const int64_t k = node_off[m + 1] - node_off[m];
+    n_cv += k * (k - 1) / 2;
+  }
+  std::vector<double> cv((size_t)std::max<int64_t>(n_cv, 1)), wd((size_t)nodes), nc(with_data ? (size_t)nodes : 0);
+  rc = nr_module_vectors(ctx.get(), n_mod, node_off.data(), idx.data(), cv.data(), wd.data(), nullptr,
+                         with_data ? nc.data() : nullptr, nullptr, nullptr);
+  if (rc) return ctx_err(rc, ctx.get());
+  // Concatenate in `modules` order (src/discProps.cpp:119-125).
+  int64_t o_cv = 0, o_n = 0;
+  for (int32_t m = 0; m < n_mod; ++m) {
+    const int64_t mi = which[m];
+    const int64_t k = node_off[m + 1] - node_off[m];
+    const int64_t kc = k * (k - 1) / 2;
+    std::memcpy(corr_out + o_cv, cv.data() + o_cv, (size_t)kc * sizeof(double));
+    std::memcpy(degree_out + o_n, wd.data() + node_off[m], (size_t)k * sizeof(double));
+    if (with_data) std::memcpy(contribution_out + o_n, nc.data() + node_off[m], (size_t)k * sizeof(double));
+    corr_len[mi] = kc;
+    degree_len[mi] = k;
+    if (with_data) contribution_len[mi] = k;
+    o_cv += kc;
+    o_n += k;
+  }
+  return NR_OK;
+}
+
+int netrep_NetProps(const double* data, const double* net, int64_t n_samples, int64_t n_nodes,
+                    const char* const* node_names, const char* const* ma_names,
+                    const char* const* ma_labels, int64_t n_assign, const char* const* modules,
+                    int64_t n_modules, double* degree_out, double* contribution_out,
+                    double* summary_out, double* coherence_out, double* avg_weight_out,
+                    int64_t* k_all_out) {
+  if (!net || !node_names || !ma_names || !ma_labels || !modules || !degree_out ||
+      !avg_weight_out || !k_all_out || n_nodes <= 0)
+    return set_err(NR_ERR_INVALID, "invalid arguments to NetProps");
+  const bool with_data = data != nullptr;
+  if (with_data && (!contribution_out || !summary_out || !coherence_out))
+    return set_err(NR_ERR_INVALID, "contribution/summary/coherence buffers required with data");
+  const double na = [] { uint64_t b = 0x7FF00000000007A2ull; double d; std::memcpy(&d, &b, 8); return d; }();
+  const NameMap node_idx = make_idx_map(node_names, n_nodes);
+  const ModMap all = make_mod_map(ma_names, ma_labels, n_assign, nullptr);  // src/properties.cpp:108
+
+  // Per module: all nodes (k_all), present nodes -> dataset index + slot.
+  std::vector<int64_t> node_off{0}, k_all(n_modules, 0), out_off(n_modules + 1, 0);
+  std::vector<int32_t> idx, slot;
+  std::vector<int64_t> which;
+  for (int64_t mi = 0; mi < n_modules; ++mi) {
+    const std::vector<std::string>* nodes = all.find(modules[mi]);
+    k_all[mi] = nodes ? (int64_t)nodes->size() : 0;
+    out_off[mi + 1] = out_off[mi] + k_all[mi];
+    if (!nodes) continue;
+    const size_t before = idx.size();
+    for (size_t j = 0; j < nodes->size(); ++j) {
+      auto it = node_idx.find((*nodes)[j]);
+      if (it == node_idx.end()) continue;
+      idx.push_back((int32_t)it->second);
+      slot.push_back((int32_t)j);
+    }
+    if (idx.size() > before) {
+      node_off.push_back((int64_t)idx.size());
+      which.push_back(mi);
+    }
+  }
+  // NA-initialised outputs (src/properties.cpp:131-139).
+  for (int64_t mi = 0; mi < n_modules; ++mi) {
+    k_all_out[mi] = k_all[mi];
+    avg_weight_out[mi] = na;
+    for (int64_t j = out_off[mi]; j < out_off[mi + 1]; ++j) {
+      degree_out[j] = na;
+      if (with_data) contribution_out[j] = na;
+    }
+    if (with_data) {
+      coherence_out[mi] = na;
+      for (int64_t s = 0; s < n_samples; ++s) summary_out[mi * n_samples + s] = na;
+    }
+  }
+  const int32_t n_mod = (int32_t)which.size();
+  if (n_mod == 0) return NR_OK;
+  CtxPtr ctx;
+  int rc = open_ctx(0, ctx);
+  if (rc) return rc;
+  std::vector<double> scaled;
+  if (with_data) {  // NetProps scales internally (src/properties.cpp:49)
+    scaled.resize((size_t)(n_samples * n_nodes));
+    rc = nr_scale(ctx.get(), data, n_samples, n_nodes, scaled.data());
+    if (rc) return ctx_err(rc, ctx.get());
+  }
+  // No correlation matrix on this path: the network doubles as the (unused)
+  // correlation operand of the interleaved dataset.
+  rc = nr_set_dataset(ctx.get(), net, net, with_data ? scaled.data() : nullptr, n_nodes, n_samples, NR_HOST);
+  if (rc) return ctx_err(rc, ctx.get());
+  const int64_t nodes = node_off.back();
+  std::vector<double> wd((size_t)nodes), aw((size_t)n_mod), nc, sp, coh;
+  if (with_data) {
+    nc.resize((size_t)nodes);
+    sp.resize((size_t)(n_mod * n_samples));
+    coh.resize((size_t)n_mod);
+  }
+  rc = nr_module_vectors(ctx.get(), n_mod, node_off.data(), idx.data(), nullptr, wd.data(), aw.data(),
+                         with_data ? nc.data() : nullptr, with_data ? sp.data() : nullptr,
+                         with_data ? coh.data() : nullptr);
+  if (rc) return ctx_err(rc, ctx.get());
+  auto na_if = [&](double x) { return std::isfinite(x) ? x : na; };
+  for (int32_t m = 0; m < n_mod; ++m) {
+    const int64_t mi = which[m];
+    avg_weight_out[mi] = aw[m];  // AverageEdgeWeight result kept as is (src/properties.cpp:160)
+    for (int64_t c = node_off[m]; c < node_off[m + 1]; ++c) {
+      const int64_t j = out_off[mi] + slot[c];  // Fill (src/utils.cpp:245-257)
+      degree_out[j] = wd[c];
+      if (with_data) contribution_out[j] = na_if(nc[c]);  // :176
+    }
+    if (with_data) {
+      coherence_out[mi] = na_if(coh[m]);  // :177-179
+      for (int64_t s = 0; s < n_samples; ++s)
+        summary_out[mi * n_samples + s] = na_if(sp[m * n_samples + s]);  // :175
+    }
+  }
+  return NR_OK;
+}
+
+int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes, double* scaled_out) {
+  if (!data || !scaled_out || n_samples <= 0 || n_nodes <= 0)
+    return set_err(NR_ERR_INVALID, "invalid arguments to Scale");
+  CtxPtr ctx;
+  int rc = open_ctx(0, ctx);
+  if (rc) return rc;
+  rc = nr_scale(ctx.get(), data, n_samples, n_nodes, scaled_out);
+  if (rc) return ctx_err(rc, ctx.get());
+  return NR_OK;
+}
+
+int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol) {
+  if (!mat || nrow < 0 || ncol < 0) return set_err(NR_ERR_INVALID, "invalid arguments to CheckFinite");
+  CtxPtr ctx;
+  int rc = open_ctx(0, ctx);
+  if (rc) return rc;
+  int ok = 1;
+  rc = nr_check_finite(ctx.get(), mat, nrow * ncol, &ok);
+  if (rc) return ctx_err(rc, ctx.get());
+  if (!ok) return set_err(NR_ERR_NONFINITE, "matrices cannot have non-finite or missing values");
+  return NR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+// Launch parameter blocks shared by kernels.hip and engine.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nr {
+
+enum { NR_IDX_PRP = 0, NR_IDX_TABLE = 1, NR_IDX_DIRECT = 2 };
+
+// Where the test column of module node c comes from.
+struct IndexSource {
+  int mode;                    // NR_IDX_*
+  uint64_t seed;               // PRP key
+  int64_t perm_base;           // global index of local permutation 0
+  uint32_t n_null;             // null-pool size
+  const int32_t* null_idx;     // [n_null] test columns of the null pool
+  const int32_t* null_pos;     // [nodes] null-pool position of each module node
+  const uint32_t* pi;          // [n_perm x n_null] explicit shuffles (TABLE)
+  const int32_t* direct_idx;   // [nodes] test column of each node (DIRECT)
+};
+
+struct NetParams {
+  const double2* pairs;        // interleaved {corr, net}, column-major n x n
+  int64_t n_nodes;
+  int symmetric;               // both matrices exactly symmetric
+  IndexSource src;
+  const int64_t* node_off;     // [n_mod + 1]
+  const int64_t* cv_off;       // [n_mod + 1] CorrVector offsets (k(k-1)/2)
+  const double* disc_cv;       // discovery CorrVector (NULL: no statistics)
+  const double* disc_wd;       // discovery weighted degree
+  const double* cv_shift;      // [n_mod] one-pass shift for the discovery corr values
+  const int32_t* mod_order;    // [n_present] module processing order (large first)
+  int32_t n_perm;              // permutations in this launch
+  int32_t k_max;
+  const int32_t* row_of;       // [n_mod] output row
+  int32_t n_rows, n_stat;
+  int32_t slot_avg_weight, slot_cor_cor, slot_cor_degree, slot_avg_cor;
+  double* out;                 // cube slice (NULL in vector mode)
+  double* cv_out;              // vector outputs (NULL unless vector mode)
+  double* wd_out;
+  double* avgw_out;            // [n_mod] average edge weight (vector mode)
+};
+
+struct ProfileParams {
+  const double* data;          // n_samples x n_nodes, column-major, scaled
+  int64_t n_samples;
+  IndexSource src;
+  const int64_t* node_off;
+  const double* disc_nc;       // discovery contribution (NULL: vector mode)
+  const int32_t* mod_order;
+  int32_t n_perm;
+  int32_t n_items;
+  int32_t k_max, kp, m_max;
+  const int32_t* row_of;
+  int32_t n_rows, n_stat;
+  int32_t slot_coherence, slot_cor_contrib, slot_avg_contrib;
+  double* out;
+  double* sp_out;              // [n_mod x n_samples] summary profiles (vector mode)
+  double* nc_out;              // [nodes] node contributions (vector mode)
+  double* coh_out;             // [n_mod] coherence (vector mode)
+  double* scratch;             // per-slot G (kp x kp) + Lanczos basis (k_max x m_max)
+  int64_t scratch_stride;
+  int* queue;                  // work-queue head, zeroed before launch
+  int* diag;                   // count of items whose Lanczos hit its step cap
+};
+
+size_t net_kernel_lds(int k_max);
+size_t profile_kernel_lds(int k_max, int m_max, int n_samples);
+hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
+hipError_t launch_profile(const ProfileParams& P, int n_slots, hipStream_t st);
+hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,
+                             hipStream_t st);
+hipError_t launch_symmetry(const double2* a, int64_t n, int* asym, hipStream_t st);
+hipError_t launch_scale(const double* in, double* out, int64_t S, int64_t N, hipStream_t st);
+hipError_t launch_finite(const double* a, int64_t n, int* nonfinite, hipStream_t st);
+hipError_t launch_export(const IndexSource& src, int64_t n_nodes_total, int32_t* out,
+                         int64_t n_perm, hipStream_t st);
+
+}  // namespace nr

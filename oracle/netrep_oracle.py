@@ -1,0 +1,302 @@
+"""CPU restatement of NetRep's permutation null-distribution path (numpy/scipy).
+
+TEST INFRASTRUCTURE ONLY. This module is the parity checker: only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import it. The product path (``netrep_amd``) never calls it.
+
+Every function restates one reference function formula by formula, citing
+the file:line it follows (paths relative to the reference tree). Where the
+reference delegates to third-party code that is absent here (Armadillo
+``svd_econ`` -> LAPACK ``dgesdd``; ``arma::cor``), the restatement calls the
+same LAPACK routine through scipy (``lapack_driver='gesdd'``) or the textbook
+definition (Pearson with n-1 normalisation).
+
+Pinning: the observed 4x7 statistics and module-1 summary profiles printed
+in vignettes/NetRep.md:301-307 and :913-958 are reproduced by
+``tests/test_oracle_golden.py`` (7-9 significant digits, the printed
+precision). RNG streams and ``statmod::permp`` are unpinned.
+
+Node order inside a module: the reference walks a Boost
+``unordered_multimap`` ``equal_range`` (src/utils.cpp:154,193), whose order
+is implementation-defined. This restatement (and the engine) use the order
+of appearance in ``moduleAssignments``. Every statistic is invariant to a
+node order applied consistently to discovery and test when the correlation
+matrix is symmetric, which is the case for correlation matrices.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.linalg
+
+STATNAMES = ["avg.weight", "coherence", "cor.cor", "cor.degree",
+             "cor.contrib", "avg.cor", "avg.contrib"]          # src/permutations.cpp:174-177
+STATNAMES_NODATA = ["avg.weight", "cor.cor", "cor.degree", "avg.cor"]  # src/permutationsNoData.cpp:156-158
+
+# R's NA_real_: a quiet NaN whose low word is 1954.
+NA_REAL_BITS = np.uint64(0x7FF00000000007A2)
+NA_REAL = np.array([NA_REAL_BITS], dtype=np.uint64).view(np.float64)[0]
+
+
+def na_fill(a):
+    """find_nonfinite -> NA_REAL (src/permutations.cpp:383-384)."""
+    a = np.array(a, dtype=np.float64, copy=True)
+    bits = a.view(np.uint64)
+    bits[~np.isfinite(a)] = NA_REAL_BITS
+    return a
+
+
+# ----------------------------------------------------------------------------
+# Statistics, src/netStats.cpp
+# ----------------------------------------------------------------------------
+
+def sort_nodes(idx):
+    """SortNodes src/netStats.cpp:23-32: returns (sorted idx, rank)."""
+    idx = np.asarray(idx)
+    order = np.argsort(idx, kind="stable")
+    rank = np.argsort(order, kind="stable")
+    return idx[order], rank
+
+
+def complete_cases(v1, v2):
+    """CompleteCases src/netStats.cpp:43-61."""
+    return np.isfinite(v1) & np.isfinite(v2)
+
+
+def _pearson(a, b):
+    n = a.size
+    if n == 0:
+        return np.nan
+    with np.errstate(invalid="ignore", divide="ignore"):
+        am = a - a.mean()
+        bm = b - b.mean()
+        den = np.sqrt((am * am).sum() * (bm * bm).sum())
+        return float((am * bm).sum() / den) if n > 1 else np.nan
+
+
+def correlation(v1, v2):
+    """Correlation src/netStats.cpp:69-83 (Pearson over complete cases)."""
+    v1 = np.asarray(v1, dtype=np.float64)
+    v2 = np.asarray(v2, dtype=np.float64)
+    cc = complete_cases(v1, v2)
+    if not cc.any():
+        return np.nan
+    return _pearson(v1[cc], v2[cc])
+
+
+def sign_aware_mean(v1, v2):
+    """SignAwareMean src/netStats.cpp:95-109: mean(sign(v1) * v2) over complete cases."""
+    v1 = np.asarray(v1, dtype=np.float64)
+    v2 = np.asarray(v2, dtype=np.float64)
+    cc = complete_cases(v1, v2)
+    if not cc.any():
+        return np.nan
+    return float(np.mean(np.sign(v1[cc]) * v2[cc]))
+
+
+def weighted_degree(net, idx_sorted):
+    """WeightedDegree src/netStats.cpp:124-144: colsum(|net[idx,idx]|) - |diag[idx]|."""
+    sub = np.abs(net[np.ix_(idx_sorted, idx_sorted)])
+    return sub.sum(axis=0) - np.abs(net[idx_sorted, idx_sorted])
+
+
+def average_edge_weight(wd):
+    """AverageEdgeWeight src/netStats.cpp:154-162 (unsigned-int pair count, :159)."""
+    k = np.uint32(len(wd))
+    with np.errstate(over="ignore"):
+        pairs = float(np.uint32(k * k - k))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return float(np.sum(wd)) / pairs if pairs != 0 else (np.nan if np.sum(wd) == 0 else np.inf)
+
+
+def corr_vector(corr, idx):
+    """CorrVector src/netStats.cpp:176-204: lower triangle, column-major over idx order."""
+    idx = np.asarray(idx)
+    n = idx.size
+    jj, ii = np.triu_indices(n, k=1)      # jj < ii, ordered by jj then ii
+    return corr[idx[ii], idx[jj]]
+
+
+def summary_profile(data, idx_sorted):
+    """SummaryProfile src/netStats.cpp:217-250: U[:,0] of svd_econ(X,'left','dc'), sign-oriented."""
+    x = data[:, idx_sorted]
+    s = data.shape[0]
+    if not np.isfinite(x).all():               # svd_econ fails on non-finite input -> NaN (:231-235)
+        return np.full(s, np.nan)
+    try:
+        u, _, _ = scipy.linalg.svd(x, full_matrices=False, lapack_driver="gesdd",
+                                   check_finite=False)
+    except (np.linalg.LinAlgError, ValueError):
+        return np.full(s, np.nan)
+    summary = u[:, 0].copy()
+    mean_obs = x.mean(axis=1)                  # :242
+    c = _pearson(mean_obs, summary)            # :243
+    if np.isfinite(c) and c < 0:               # orientation == -1 (:245)
+        summary *= -1
+    return summary
+
+
+def node_contribution(data, idx_sorted, summary):
+    """NodeContribution src/netStats.cpp:265-280: cor(X[:, j], summary) per column."""
+    x = data[:, idx_sorted]
+    return np.array([_pearson(x[:, j], summary) for j in range(x.shape[1])])
+
+
+def module_coherence(nc):
+    """ModuleCoherence src/netStats.cpp:293-305: mean(NC^2) over finite NC."""
+    nc = np.asarray(nc, dtype=np.float64)
+    f = np.isfinite(nc)
+    if not f.any():
+        return np.nan
+    return float(np.mean(nc[f] ** 2))
+
+
+def scale(data):
+    """Scale src/scale.cpp:14-25: per column (x - mean) / sd (n-1)."""
+    data = np.asarray(data, dtype=np.float64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return (data - data.mean(axis=0)) / data.std(axis=0, ddof=1)
+
+
+# ----------------------------------------------------------------------------
+# Index derivation, src/utils.cpp
+# ----------------------------------------------------------------------------
+
+class ModuleIndex:
+    """Name maps of src/utils.cpp:5-65,108-162 resolved to integer index sets.
+
+    module_assignments: dict-like sequence of (node name, module label),
+    in the order of R's named vector ``moduleAssignments``.
+    """
+
+    def __init__(self, node_names, labels, test_names, modules, null="overlap"):
+        node_names = [str(n) for n in node_names]
+        labels = [str(v) for v in labels]
+        test_names = [str(n) for n in test_names]
+        self.modules = [str(m) for m in modules]
+        t_idx = {n: i for i, n in enumerate(test_names)}                 # MakeIdxMap :5-11
+        present = {}                                                      # MakeModMap(.., tIdx) :47-65
+        for name, lab in zip(node_names, labels):
+            if name in t_idx:
+                present.setdefault(lab, []).append(name)
+        self.present_nodes = present
+        self.mods_present = [m for m in self.modules if m in present]    # permutations.cpp:196-201
+        self.test_idx = {m: np.array([t_idx[n] for n in present[m]], dtype=np.int64)
+                         for m in self.mods_present}                      # GetNodeIdx :147-162
+        valid = node_names if null == "overlap" else test_names          # permutations.cpp:319-323
+        null_idx, null_map = [], {}
+        for name in valid:                                                # MakeNullMap :108-136
+            if name in t_idx:
+                null_map[name] = len(null_idx)
+                null_idx.append(t_idx[name])
+        self.null_idx = np.array(null_idx, dtype=np.int64)
+        self.null_pos = {m: np.array([null_map[n] for n in present[m]], dtype=np.int64)
+                         for m in self.mods_present}
+
+    def disc_idx(self, disc_names):
+        d_idx = {str(n): i for i, n in enumerate(disc_names)}
+        return {m: np.array([d_idx[n] for n in self.present_nodes[m]], dtype=np.int64)
+                for m in self.mods_present}
+
+    def random_idx(self, pi):
+        """GetRandomIdx src/utils.cpp:176-201 for one permutation table pi."""
+        return {m: self.null_idx[pi[self.null_pos[m]]] for m in self.mods_present}
+
+
+# ----------------------------------------------------------------------------
+# Drivers
+# ----------------------------------------------------------------------------
+
+def intermediate_properties(d_data, d_corr, d_net, disc_idx, with_data=True):
+    """IntermediateProperties[NoData] src/discProps.cpp:92-122 / :215-236."""
+    out = {"degree": {}, "corr": {}}
+    if with_data:
+        out["contribution"] = {}
+    for m, idx in disc_idx.items():
+        out["corr"][m] = corr_vector(d_corr, idx)
+        srt, rank = sort_nodes(idx)
+        out["degree"][m] = weighted_degree(d_net, srt)[rank]
+        if with_data:
+            sp = summary_profile(d_data, srt)
+            out["contribution"][m] = node_contribution(d_data, srt, sp)[rank]
+    return out
+
+
+def module_stats(disc, m, t_data, t_corr, t_net, idx, with_data=True):
+    """Body of calculateNulls src/permutations.cpp:71-101 (or :66-85 no data)."""
+    t_cv = corr_vector(t_corr, idx)                               # :75
+    srt, rank = sort_nodes(idx)                                   # :79
+    t_wd = weighted_degree(t_net, srt)[rank]                      # :81-82
+    d_cv, d_wd = disc["corr"][m], disc["degree"][m]
+    if not with_data:
+        return [average_edge_weight(t_wd), correlation(d_cv, t_cv),
+                correlation(d_wd, t_wd), sign_aware_mean(d_cv, t_cv)]
+    t_sp = summary_profile(t_data, srt)                           # :85
+    t_nc = node_contribution(t_data, srt, t_sp)[rank]             # :88-90
+    d_nc = disc["contribution"][m]
+    return [average_edge_weight(t_wd),                            # :95
+            module_coherence(t_nc),                               # :96
+            correlation(d_cv, t_cv),                              # :97
+            correlation(d_wd, t_wd),                              # :98
+            correlation(d_nc, t_nc),                              # :99
+            sign_aware_mean(d_cv, t_cv),                          # :100
+            sign_aware_mean(d_nc, t_nc)]                          # :101
+
+
+def permutation_procedure(disc, t_data, t_corr, t_net, mi: ModuleIndex, pis,
+                          with_data=True):
+    """PermutationProcedure[NoData] src/permutations.cpp:160-409 with explicit pi tables.
+
+    pis: array (P, n_null) of null-pool permutations (pi[p][q] = source
+    position; the shuffled nullIdx of permutation p is null_idx[pi[p]]).
+    Returns (nulls[M, S, P], observed[M, S]) with NA_REAL fill, R layout.
+    """
+    n_stat = 7 if with_data else 4
+    n_mod = len(mi.modules)
+    row = {m: i for i, m in enumerate(mi.modules)}
+    obs = np.full((n_mod, n_stat), np.nan)
+    for m in mi.mods_present:                                     # :246-285
+        obs[row[m]] = module_stats(disc, m, t_data, t_corr, t_net, mi.test_idx[m], with_data)
+    pis = np.asarray(pis)
+    nulls = np.full((n_mod, n_stat, pis.shape[0]), np.nan)
+    for p in range(pis.shape[0]):                                 # :62
+        ridx = mi.random_idx(pis[p])
+        for m in mi.mods_present:                                 # :64
+            nulls[row[m], :, p] = module_stats(disc, m, t_data, t_corr, t_net, ridx[m], with_data)
+    return na_fill(nulls), na_fill(obs)
+
+
+def net_props(data, net, node_names, module_nodes, modules):
+    """NetProps src/properties.cpp:41-156 (data=None -> NetPropsNoData :190-273).
+
+    module_nodes: {label: [node names in moduleAssignments order]}.
+    Returns {label: dict(summary, contribution, coherence, degree, avgWeight)}.
+    """
+    scaled = scale(data) if data is not None else None           # :49
+    n_idx = {str(n): i for i, n in enumerate(node_names)}
+    n_samples = data.shape[0] if data is not None else 0
+    res = {}
+    for m in modules:
+        names = module_nodes[m]
+        pres = [i for i, n in enumerate(names) if n in n_idx]     # propIdx :104
+        node_idx = np.array([n_idx[names[i]] for i in pres], dtype=np.int64)
+        degree = np.full(len(names), np.nan)
+        contribution = np.full(len(names), np.nan)
+        summary = np.full(n_samples, np.nan)
+        avg_weight = coherence = np.nan
+        if node_idx.size > 0:
+            srt, rank = sort_nodes(node_idx)
+            wd = weighted_degree(net, srt)[rank]
+            avg_weight = average_edge_weight(wd)
+            degree[pres] = wd
+            if scaled is not None:
+                sp = summary_profile(scaled, srt)
+                nc = node_contribution(scaled, srt, sp)[rank]
+                coherence = module_coherence(nc)
+                contribution[pres] = nc
+                summary = sp
+        entry = {"degree": na_fill(degree), "avgWeight": na_fill([avg_weight])[0]}
+        if data is not None:
+            entry.update(summary=na_fill(summary), contribution=na_fill(contribution),
+                         coherence=na_fill([coherence])[0])
+        res[m] = entry
+    return res

@@ -1,0 +1,57 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP engine)")
+
+
+def _load(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
+
+
+@pytest.fixture(scope="session")
+def bundled():
+    return _load("netrep_bundled.npz")
+
+
+@pytest.fixture(scope="session")
+def bundled_expected():
+    return _load("bundled_expected.npz")
+
+
+@pytest.fixture(scope="session")
+def asym():
+    return _load("asym_case.npz")
+
+
+# Tolerance of the statistics against the oracle (fp64, BASELINE.json north star:
+# "within 1e-10 relative"). Correlation-type statistics of the null are centred
+# on 0, so relative error is measured against max(|expected|, 1e-2): a value
+# of 1e-6 must still agree to 1e-12 absolute.
+RTOL = 1e-10
+FLOOR = 1e-2
+
+
+def assert_stats_close(got, exp, rtol=RTOL, floor=FLOOR, what=""):
+    got = np.asarray(got, dtype=np.float64)
+    exp = np.asarray(exp, dtype=np.float64)
+    assert got.shape == exp.shape, (what, got.shape, exp.shape)
+    gf, ef = np.isfinite(got), np.isfinite(exp)
+    assert (gf == ef).all(), f"{what}: NA pattern differs at {np.argwhere(gf != ef)[:5].tolist()}"
+    # NA must be R's NA_real_ bit pattern where the oracle has it
+    gb = got.view(np.uint64)[~gf]
+    eb = exp.view(np.uint64)[~ef]
+    assert (gb == eb).all(), f"{what}: NA bit pattern differs"
+    err = np.abs(got[gf] - exp[ef]) / np.maximum(np.abs(exp[ef]), floor)
+    if err.size:
+        assert err.max() <= rtol, f"{what}: max scaled error {err.max():.3e} at {np.argmax(err)}"
+    return float(err.max()) if err.size else 0.0
