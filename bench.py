@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--cpu-baseline-perms", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--stamps", action="store_true",
+                    help="diagnostic run: per-phase cycle stamps in the profile kernel")
     return ap.parse_args()
 
 
@@ -123,7 +125,7 @@ def build_case(cfg, world, rank, local, seed):
     torch.cuda.empty_cache()
     return eng, lay, dict(node_off=node_off, idx=idx, disc_cv=disc_cv, disc_wd=disc_wd,
                           disc_nc=disc_nc, with_data=with_data, n_samples=n_samples,
-                          n_nodes=n_nodes, t_bcast=t_bcast), host
+                          n_nodes=n_nodes, t_bcast=t_bcast, symmetric=eng.symmetric()), host
 
 
 def roofline_terms(sizes, n_samples, with_data):
@@ -181,6 +183,8 @@ def main():
     eng.synchronize()
     eng.set_timing(True)
     eng.reset_timing()
+    if args.stamps:
+        eng.set_stamps(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -200,6 +204,9 @@ def main():
     ms0, l0, _ = eng.timing(0)
     ms1, l1, _ = eng.timing(1)
     finite = float(np.isfinite(nulls).mean())
+    diag = eng.diagnostics()
+    if args.stamps:
+        diag["stamps_cycles"] = eng.stamps()
 
     if rank == 0:
         total_perms = world * K * B
@@ -252,6 +259,8 @@ def main():
             "cpu_baseline": cpu,
             "finite_fraction": finite,
             "broadcast_s": meta["t_bcast"],
+            "symmetric_matrices": meta["symmetric"],
+            "eigen_diagnostics": diag,
         }
         print(json.dumps(line))
     if world > 1:

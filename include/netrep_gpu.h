@@ -152,7 +152,17 @@ int nr_set_timing(nr_ctx* ctx, int enable);
 int nr_get_timing(nr_ctx* ctx, int kernel, double* total_ms, int64_t* launches,
                   int64_t* items);
 int nr_reset_timing(nr_ctx* ctx);
+/* Summary-profile eigen-solver counters since the last nr_reset_timing:
+ * items solved, Lanczos steps taken, items that reached the step cap. */
+int nr_get_diagnostics(nr_ctx* ctx, int64_t* eig_items, int64_t* eig_steps,
+                       int64_t* eig_cap_hits);
 int nr_synchronize(nr_ctx* ctx);
+/* Diagnostics: per-phase shader-cycle stamps of the summary-profile kernel,
+ * summed over workgroups (0 index, 1 Gram, 2 Lanczos vector work, 3 Lanczos
+ * matvec, 4 reorthogonalisation, 5 tail). Off by default; a run with stamps
+ * on is a measurement run, not a timed one. */
+int nr_set_stamps(nr_ctx* ctx, int enable);
+int nr_get_stamps(nr_ctx* ctx, uint64_t* cycles);
 
 /* ---- reference-interface layer ----------------------------------------- */
 /* Names are arrays of NUL-terminated strings. moduleAssignments is the named

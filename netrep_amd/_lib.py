@@ -75,7 +75,10 @@ SIGNATURES = {
     "nr_set_timing": (_int, [_p, _int]),
     "nr_get_timing": (_int, [_p, _int, _dp, _i64p, _i64p]),
     "nr_reset_timing": (_int, [_p]),
+    "nr_get_diagnostics": (_int, [_p, _i64p, _i64p, _i64p]),
     "nr_synchronize": (_int, [_p]),
+    "nr_set_stamps": (_int, [_p, _int]),
+    "nr_get_stamps": (_int, [_p, C.POINTER(C.c_uint64)]),
     "netrep_PermutationProcedure": (_int, [C.POINTER(DiscProps), _dp, _dp, _dp, _i64, _i64, _strv,
                                            _strv, _strv, _i64, _strv, _i64, _i64, _i32, C.c_char_p,
                                            _i32, _u64, _u32p, _dp, _dp]),

@@ -73,13 +73,14 @@ struct nr_ctx {
   size_t pi_cap = 0;
   double* d_scratch = nullptr;
   size_t scratch_cap = 0;
-  int* d_counters = nullptr;  // [0] queue head, [1] lanczos cap hits, [2] flag
+  int* d_counters = nullptr;  // [0] queue head, [1..3] lanczos diagnostics, [4] flag
   int64_t batch = 0;          // 0 = automatic
 
   std::atomic<int64_t> done{0}, total{0};
   std::atomic<bool> cancel{false};
 
   bool timing = false;
+  unsigned long long* d_stamps = nullptr;  // phase stamps (nr_set_stamps)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   DeviceTimer timers[2];
 };
@@ -152,19 +153,28 @@ int fill_na(nr_ctx* ctx, double* d, int64_t n) {
 
 int n_stat_of(const nr_ctx* ctx) { return ctx->d_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA; }
 
-int profile_slots(const nr_ctx* ctx, int64_t n_items) {
+int profile_m_max(int k_max) { return std::min(k_max, 160); }
+// Leading dimension of the per-slot Gram: k module columns + the ones column,
+// padded to a 32-column super-tile.
+int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
+
+// Persistent profile workgroups: as many per CU as LDS allows (at most 4).
+int profile_slots(const nr_ctx* ctx, int64_t n_items, int k_max, int n_samples) {
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-  const int64_t slots = std::min<int64_t>(n_items, (int64_t)dev_cu * 2);
+  const size_t lds = nr::profile_kernel_lds(k_max, profile_m_max(k_max), n_samples);
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / lds));
+  const int64_t slots = std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu);
   return (int)std::max<int64_t>(slots, 1);
 }
 
-int profile_m_max(int k_max) { return std::min(k_max, 512); }
-int round16(int k) { return (k + 15) / 16 * 16; }
+bool profile_fits(int k_max, int n_samples) {
+  return nr::profile_kernel_lds(k_max, profile_m_max(k_max), n_samples) <= 160 * 1024;
+}
 
 int ensure_scratch(nr_ctx* ctx, int slots, int k_max, int64_t* stride_out) {
-  const int kp = round16(k_max);
-  const int64_t stride = (int64_t)kp * kp + (int64_t)k_max * profile_m_max(k_max);
+  const int64_t ld = gram_ld(k_max);
+  const int64_t stride = ld * ld + (int64_t)k_max * profile_m_max(k_max);
   *stride_out = stride;
   return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(stride * slots));
 }
@@ -236,7 +246,9 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   timer_end(ctx, 0, n_items);
 
   if (data) {
-    const int slots = profile_slots(ctx, n_items);
+    if (!profile_fits(ctx->k_max, (int)ctx->n_samples))
+      return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
+    const int slots = profile_slots(ctx, n_items, ctx->k_max, (int)ctx->n_samples);
     int64_t stride = 0;
     rc = ensure_scratch(ctx, slots, ctx->k_max, &stride);
     if (rc) return rc;
@@ -251,7 +263,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.n_perm = (int32_t)n_perm;
     pp.n_items = (int32_t)n_items;
     pp.k_max = ctx->k_max;
-    pp.kp = round16(ctx->k_max);
+    pp.ld = gram_ld(ctx->k_max);
     pp.m_max = profile_m_max(ctx->k_max);
     pp.row_of = ctx->d_row_of;
     pp.n_rows = ctx->n_rows;
@@ -264,6 +276,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.scratch_stride = stride;
     pp.queue = ctx->d_counters;
     pp.diag = ctx->d_counters + 1;
+    pp.stamps = ctx->d_stamps;
     timer_begin(ctx, 1);
     NR_HIP(ctx, nr::launch_profile(pp, slots, ctx->stream));
     timer_end(ctx, 1, n_items);
@@ -404,6 +417,7 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   dfree(ctx->d_pi);
   dfree(ctx->d_scratch);
   dfree(ctx->d_counters);
+  dfree(ctx->d_stamps);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   for (auto& ev : ctx->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -453,10 +467,10 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
     (void)hipFree(tn);
     if (e != hipSuccess) return hip_fail(ctx, e, "dataset upload");
   }
-  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 2, 0, sizeof(int), ctx->stream));
-  NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 2, ctx->stream));
+  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 4, 0, sizeof(int), ctx->stream));
+  NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 4, ctx->stream));
   int asym = 0;
-  NR_HIP(ctx, hipMemcpyAsync(&asym, ctx->d_counters + 2, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  NR_HIP(ctx, hipMemcpyAsync(&asym, ctx->d_counters + 4, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   if (data) {
     const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
     NR_HIP(ctx, hipMalloc((void**)&ctx->d_data, bytes));
@@ -668,7 +682,11 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
     np.avgw_out = d_aw;
     e = nr::launch_net(np, n_mod, ctx->stream);
     if (e == hipSuccess && ctx->d_data && (contribution || summary || coherence)) {
-      const int slots = profile_slots(ctx, n_mod);
+      if (!profile_fits(kmax, (int)S)) {
+        rc = fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
+        break;
+      }
+      const int slots = profile_slots(ctx, n_mod, kmax, (int)S);
       int64_t stride = 0;
       if ((rc = ensure_scratch(ctx, slots, kmax, &stride))) break;
       e = hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream);
@@ -681,7 +699,7 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
       pp.n_perm = 1;
       pp.n_items = n_mod;
       pp.k_max = kmax;
-      pp.kp = round16(kmax);
+      pp.ld = gram_ld(kmax);
       pp.m_max = profile_m_max(kmax);
       pp.sp_out = d_sp;
       pp.nc_out = d_nc;
@@ -734,15 +752,15 @@ int nr_check_finite(nr_ctx* ctx, const double* mat, int64_t n_elem, int* all_fin
   const int64_t chunk = std::min<int64_t>(n_elem, (int64_t)1 << 26);
   double* d = nullptr;
   NR_HIP(ctx, hipMalloc((void**)&d, (size_t)chunk * sizeof(double)));
-  hipError_t e = hipMemsetAsync(ctx->d_counters + 2, 0, sizeof(int), ctx->stream);
+  hipError_t e = hipMemsetAsync(ctx->d_counters + 4, 0, sizeof(int), ctx->stream);
   for (int64_t o = 0; o < n_elem && e == hipSuccess; o += chunk) {
     const int64_t len = std::min(chunk, n_elem - o);
     e = hipMemcpyAsync(d, mat + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = nr::launch_finite(d, len, ctx->d_counters + 2, ctx->stream);
+    if (e == hipSuccess) e = nr::launch_finite(d, len, ctx->d_counters + 4, ctx->stream);
   }
   int bad = 0;
   if (e == hipSuccess)
-    e = hipMemcpyAsync(&bad, ctx->d_counters + 2, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    e = hipMemcpyAsync(&bad, ctx->d_counters + 4, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   (void)hipFree(d);
   if (e != hipSuccess) return hip_fail(ctx, e, "check finite");
@@ -787,6 +805,40 @@ int nr_reset_timing(nr_ctx* ctx) {
   if (!ctx) return NR_ERR_INVALID;
   ctx->timers[0] = DeviceTimer();
   ctx->timers[1] = DeviceTimer();
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 1, 0, 3 * sizeof(int), ctx->stream));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return NR_OK;
+}
+
+int nr_set_stamps(nr_ctx* ctx, int enable) {
+  if (!ctx) return NR_ERR_INVALID;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  if (enable && !ctx->d_stamps) {
+    NR_HIP(ctx, hipMalloc((void**)&ctx->d_stamps, 8 * sizeof(unsigned long long)));
+  }
+  if (enable) NR_HIP(ctx, hipMemset(ctx->d_stamps, 0, 8 * sizeof(unsigned long long)));
+  if (!enable) dfree(ctx->d_stamps);
+  return NR_OK;
+}
+
+int nr_get_stamps(nr_ctx* ctx, uint64_t* cycles) {
+  if (!ctx || !cycles) return NR_ERR_INVALID;
+  if (!ctx->d_stamps) return fail(ctx, NR_ERR_INVALID, "stamps not enabled");
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipMemcpy(cycles, ctx->d_stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return NR_OK;
+}
+
+int nr_get_diagnostics(nr_ctx* ctx, int64_t* eig_items, int64_t* eig_steps, int64_t* eig_cap_hits) {
+  if (!ctx) return NR_ERR_INVALID;
+  int h[3] = {0, 0, 0};
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipMemcpyAsync(h, ctx->d_counters + 1, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (eig_cap_hits) *eig_cap_hits = h[0];
+  if (eig_items) *eig_items = h[1];
+  if (eig_steps) *eig_steps = h[2];
   return NR_OK;
 }
 

@@ -50,7 +50,8 @@ struct ProfileParams {
   const int32_t* mod_order;
   int32_t n_perm;
   int32_t n_items;
-  int32_t k_max, kp, m_max;
+  int32_t k_max, m_max;
+  int32_t ld;                  // leading dimension of the per-slot Gram
   const int32_t* row_of;
   int32_t n_rows, n_stat;
   int32_t slot_coherence, slot_cor_contrib, slot_avg_contrib;
@@ -58,10 +59,11 @@ struct ProfileParams {
   double* sp_out;              // [n_mod x n_samples] summary profiles (vector mode)
   double* nc_out;              // [nodes] node contributions (vector mode)
   double* coh_out;             // [n_mod] coherence (vector mode)
-  double* scratch;             // per-slot G (kp x kp) + Lanczos basis (k_max x m_max)
+  double* scratch;             // per-slot Gram (ld x ld) + Lanczos basis (k_max x m_max)
   int64_t scratch_stride;
   int* queue;                  // work-queue head, zeroed before launch
-  int* diag;                   // count of items whose Lanczos hit its step cap
+  int* diag;                   // [0] Lanczos step-cap hits, [1] items, [2] Lanczos steps
+  unsigned long long* stamps;  // [8] per-phase shader cycles (diagnostics; NULL = off)
 };
 
 size_t net_kernel_lds(int k_max);

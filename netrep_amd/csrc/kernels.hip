@@ -100,8 +100,12 @@ __global__ void __launch_bounds__(NR_BS)
 module_net_kernel(NetParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* red = reinterpret_cast<double*>(smem);                    // 8 * NR_WAVES
-  double* wd = red + 8 * NR_WAVES;                                  // [k]
-  uint32_t* idx = reinterpret_cast<uint32_t*>(wd + P.k_max);        // [k]
+  double* wd = red + 8 * NR_WAVES;                                  // [NR_WAVES][k_max]
+  uint32_t* idx = reinterpret_cast<uint32_t*>(wd + NR_WAVES * P.k_max);  // [k]
+  // Each wave accumulates the weighted degrees into its own copy: the pair ->
+  // (wave, lane, iteration) assignment is fixed, so the sums are bitwise
+  // reproducible; the copies are added in wave order afterwards.
+  double* wdw = wd + (threadIdx.x >> 6) * P.k_max;
 
   const int64_t item = blockIdx.x;
   const int64_t mslot = item / P.n_perm;
@@ -116,7 +120,8 @@ module_net_kernel(NetParams P) {
 
   for (int64_t c = tid; c < k; c += NR_BS) {
     idx[c] = node_index(P.src, key, p_local, off + c);
-    wd[c] = 0.0;
+#pragma unroll
+    for (int w = 0; w < NR_WAVES; ++w) wd[w * P.k_max + c] = 0.0;
   }
   __syncthreads();
 
@@ -156,8 +161,8 @@ module_net_kernel(NetParams P) {
       if (jjs[u] < 0) continue;
       const double y = e[u].x;
       if (P.cv_out) P.cv_out[cvo + v0 + (int64_t)u * NR_BS] = y;
-      atomicAdd(&wd[jjs[u]], fabs(e[u].y));     // column idx[jj] gains row idx[ii]
-      atomicAdd(&wd[iis[u]], fabs(e2[u]));      // column idx[ii] gains row idx[jj]
+      atomicAdd(&wdw[jjs[u]], fabs(e[u].y));    // column idx[jj] gains row idx[ii]
+      atomicAdd(&wdw[iis[u]], fabs(e2[u]));     // column idx[ii] gains row idx[jj]
       const double xv = x[u];
       if (isfinite(xv) && isfinite(y)) {        // CompleteCases src/netStats.cpp:43-61
         const double dx = xv - xs, dy = y - ys;
@@ -172,6 +177,13 @@ module_net_kernel(NetParams P) {
     }
   }
   block_sums<7>(acc, red);
+  for (int64_t c = tid; c < k; c += NR_BS) {
+    double s = wd[c];
+#pragma unroll
+    for (int w = 1; w < NR_WAVES; ++w) s += wd[w * P.k_max + c];
+    wd[c] = s;
+  }
+  __syncthreads();
 
   // Weighted degree statistics: two-pass over the k values held in LDS.
   const int64_t woff = off;
@@ -331,18 +343,226 @@ __device__ void tri_eigenvector(const double* alpha, const double* beta, int n, 
   }
 }
 
-__global__ void __launch_bounds__(NR_BS)
+// w = G x over the leading k x k block of G (column-major, leading dimension
+// ld, symmetric, both triangles stored). Waves take contiguous column ranges,
+// lanes own rows (RB per 64*RB-row block), U columns are loaded ahead per
+// lane; no cross-lane reduction. part[wave][r] is written (not accumulated).
+template <int RB, int U>
+__device__ __forceinline__ void matvec_part(const double* __restrict__ G, int ld, int k,
+                                            const double* x, double* part, int kstride,
+                                            int wave, int lane) {
+  const int cpw = (k + NR_WAVES - 1) / NR_WAVES;
+  const int c0 = wave * cpw;
+  const int c1 = min(k, c0 + cpw);
+  for (int rb = 0; rb < k; rb += 64 * RB) {
+    double acc[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) acc[i] = 0.0;
+    int c = c0;
+    for (; c + U <= c1; c += U) {
+      double g[U][RB];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int r = rb + lane + 64 * i;
+          g[u][i] = r < k ? G[r + (int64_t)(c + u) * ld] : 0.0;
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double xc = x[c + u];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i] += g[u][i] * xc;
+      }
+    }
+    for (; c < c1; ++c) {
+      const double xc = x[c];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int r = rb + lane + 64 * i;
+        if (r < k) acc[i] += G[r + (int64_t)c * ld] * xc;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = rb + lane + 64 * i;
+      if (r < k) part[wave * kstride + r] = c1 > c0 ? acc[i] : 0.0;
+    }
+  }
+}
+
+// out = G x; returns (block-wide) sum_r y[r] * out[r] when y != NULL.
+__device__ __forceinline__ double matvec(const double* __restrict__ G, int ld, int k, const double* x,
+                                         double* out, double* part, int kstride, const double* y,
+                                         double* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  matvec_part<2, 4>(G, ld, k, x, part, kstride, wave, lane);
+  __syncthreads();
+  double d[1] = {0.0};
+  for (int r = threadIdx.x; r < k; r += NR_BS) {
+    double s = part[r];
+#pragma unroll
+    for (int w = 1; w < NR_WAVES; ++w) s += part[w * kstride + r];
+    out[r] = s;
+    if (y) d[0] += y[r] * s;
+  }
+  block_sums<1>(d, red);
+  return d[0];
+}
+
+// Lanczos reorthogonalisation against the stored basis Q (column-major k x n)
+// of the 3-term-corrected vector z = w - a q - b qprev: z is formed in LDS
+// once, h = Q^T z with four dots in flight per wave, then w <- z - Q h.
+// Returns |w|^2.
+__device__ __forceinline__ double reorthogonalise(const double* __restrict__ Q, int k, int n, double* w,
+                                                  const double* q, const double* qprev, double a,
+                                                  double b, double* h, double* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = threadIdx.x; c < k; c += NR_BS) w[c] = w[c] - a * q[c] - b * qprev[c];
+  __syncthreads();
+  for (int i0 = 4 * wave; i0 < n; i0 += 4 * NR_WAVES) {
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int c = lane; c < k; c += 64) {
+      const double z = w[c];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (i0 + t < n) s[t] += Q[(int64_t)(i0 + t) * k + c] * z;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) s[t] += __shfl_xor(s[t], o, 64);
+    if (lane < 4 && i0 + lane < n) h[i0 + lane] = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
+  }
+  __syncthreads();
+  double nrm[1] = {0.0};
+  for (int c = threadIdx.x; c < k; c += NR_BS) {
+    double acc = 0.0;
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+      const double q0 = Q[(int64_t)i * k + c], q1 = Q[(int64_t)(i + 1) * k + c];
+      const double q2 = Q[(int64_t)(i + 2) * k + c], q3 = Q[(int64_t)(i + 3) * k + c];
+      acc += h[i] * q0 + h[i + 1] * q1 + h[i + 2] * q2 + h[i + 3] * q3;
+    }
+    for (; i < n; ++i) acc += h[i] * Q[(int64_t)i * k + c];
+    const double z = w[c] - acc;
+    w[c] = z;
+    nrm[0] += z * z;
+  }
+  block_sums<1>(nrm, red);
+  return nrm[0];
+}
+
+// Loads one 4-row group of an operand column for the Gram MFMA: rows
+// s .. s+3 of a data column, of the virtual all-ones column, or zeros.
+__device__ __forceinline__ void load4(const double* __restrict__ col, bool ones, int s, int S,
+                                      double (&v)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int r = s + t;
+    v[t] = r < S ? (col ? col[r] : (ones ? 1.0 : 0.0)) : 0.0;
+  }
+}
+
+// G = [X 1]^T [X 1] over the k module columns of X (S x N, column-major) plus a
+// virtual all-ones column at index k, so row k of G holds the column sums;
+// both triangles stored, leading dimension ld >= round32(k + 1). 32 x 32 super-tiles (2 x 2 MFMA tiles of v_mfma_f64_16x16x4_f64) per
+// wave; each lane feeds 4 consecutive rows of every operand column per 16-row
+// step (the K order of the dot products is permuted, identically for both
+// operands). Returns per-lane partial of 1^T G 1 over the X block and a
+// non-finite flag.
+__device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* idx, int k,
+                          double* __restrict__ G, int ld, double& g1sum, int& bad) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int kc = k + 1;
+  const int T2 = (kc + 31) / 32;
+  const int nsup = T2 * (T2 + 1) / 2;
+  for (int t = wave; t < nsup; t += NR_WAVES) {
+    int I2 = 0, rem = t;
+    while (rem >= T2 - I2) { rem -= T2 - I2; ++I2; }
+    const int J2 = I2 + rem;
+    int cols[4] = {I2 * 32 + i16, I2 * 32 + 16 + i16, J2 * 32 + i16, J2 * 32 + 16 + i16};
+    const double* ptr[4];
+    bool ones[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      ptr[o] = cols[o] < k ? X + (int64_t)idx[cols[o]] * S : nullptr;
+      ones[o] = cols[o] == k;
+    }
+    nr_f64x4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+    double cur[4][4], nxt[4][4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], 4 * kk, S, cur[o]);
+    for (int s0 = 0; s0 < S; s0 += 16) {
+      const int sn = s0 + 16 + 4 * kk;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], sn, S, nxt[o]);
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[2][q], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[3][q], acc[1][1], 0, 0, 0);
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+    }
+    const double wgt = (I2 == J2) ? 1.0 : 2.0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // D[row = (lane>>4) + 4r][col = lane & 15] (f64 MFMA C/D map)
+          const int gi = I2 * 32 + 16 * a + kk + 4 * r;
+          const int gj = J2 * 32 + 16 * b + i16;
+          const double val = acc[a][b][r];
+          G[gi + (int64_t)gj * ld] = val;
+          G[gj + (int64_t)gi * ld] = val;
+          if (gi < k && gj < k) g1sum += wgt * val;
+        }
+  }
+}
+
+// Phase stamps (diagnostics only: active when P.stamps != NULL, a separate
+// measurement run; no stamp executes otherwise). Thread 0 accumulates shader
+// cycles per phase between the barriers that already delimit the phases.
+__device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memtime(); }
+#define NR_STAMP(slot)                                                          \
+  do {                                                                          \
+    if (P.stamps && threadIdx.x == 0) {                                         \
+      const uint64_t t_ = nr_clock();                                           \
+      atomicAdd((unsigned long long*)&P.stamps[slot], (unsigned long long)(t_ - t_mark)); \
+      t_mark = t_;                                                              \
+    }                                                                           \
+  } while (0)
+
+__global__ void __launch_bounds__(NR_BS, 3)
 module_profile_kernel(ProfileParams P) {
+  uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int kmax = P.k_max, mmax = P.m_max, S = (int)P.n_samples;
   double* red = reinterpret_cast<double*>(smem);        // 8 * NR_WAVES
-  double* q = red + 8 * NR_WAVES;                        // [kmax]
-  double* w = q + kmax;                                  // [kmax]
+  double* q = red + 8 * NR_WAVES;                        // [kmax] current Lanczos vector
+  double* qprev = q + kmax;                              // [kmax] previous Lanczos vector
+  double* w = qprev + kmax;                              // [kmax]
   double* vv = w + kmax;                                 // [kmax] Ritz vector
   double* gv = vv + kmax;                                // [kmax] G v
   double* colm = gv + kmax;                              // [kmax] column means
-  double* mo = colm + kmax;                              // [S] meanObs (row means)
-  double* alpha = mo + S;                                // [mmax]
+  double* part = colm + kmax;                            // [NR_WAVES * kmax] matvec partials
+  double* alpha = part + NR_WAVES * kmax;                // [mmax]
   double* beta = alpha + mmax;                           // [mmax]
   double* h = beta + mmax;                               // [mmax]
   double* ty = h + mmax;                                 // [mmax]
@@ -353,10 +573,11 @@ module_profile_kernel(ProfileParams P) {
   __shared__ int s_done;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;
-  const int kp = P.kp;
-  double* Q = G + (int64_t)kp * kp;
+  double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;   // Gram (ld x ld)
+  const int ld = P.ld;
+  double* Q = G + (int64_t)ld * ld;                                 // Lanczos basis
   const double* __restrict__ X = P.data;
+  const double Sd = (double)S;
 
   for (;;) {
     if (tid == 0) s_item = atomicAdd(P.queue, 1);
@@ -376,110 +597,52 @@ module_profile_kernel(ProfileParams P) {
     for (int c = tid; c < k; c += NR_BS) idx[c] = node_index(P.src, key, p_local, off + c);
     if (tid == 0) s_flag = 0;
     __syncthreads();
+    NR_STAMP(0);  // queue + index derivation
 
-    // Column means + finiteness (svd_econ refuses non-finite input:
-    // src/netStats.cpp:229-235 -> all-NaN summary).
-    for (int c = tid; c < k; c += NR_BS) {
-      const double* col = X + (int64_t)idx[c] * S;
-      double s = 0.0;
-      bool fin = true;
-      for (int r = 0; r < S; ++r) {
-        const double xv = col[r];
-        fin &= isfinite(xv);
-        s += xv;
-      }
-      colm[c] = s / (double)S;
-      if (!fin) atomicOr(&s_flag, 1);
-    }
-    // Row means of the module block (meanObs, src/netStats.cpp:242).
-    for (int r = tid; r < S; r += NR_BS) {
-      double s = 0.0;
-      for (int c = 0; c < k; ++c) s += X[(int64_t)idx[c] * S + r];
-      mo[r] = s / (double)k;
-    }
-    __syncthreads();
-    const bool bad = s_flag != 0;
+    // ---- Gram [X 1]^T [X 1] on the matrix cores ----
+    double g1[1] = {0.0};
+    int bad = 0;
+    gram_mfma(X, S, idx, k, G, ld, g1[0], bad);
+    if (bad) atomicOr(&s_flag, 1);
+    block_sums<1>(g1, red);      // barriers also publish G to the whole workgroup
+    const double ones_g_ones = g1[0];
+    NR_STAMP(1);  // Gram
+    // svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235)
+    const bool nonfinite = s_flag != 0;
 
-    double stat_coh = nr_nan(), stat_cc = nr_nan(), stat_ac = nr_nan();
-    if (!bad) {
-      // ---- Gram G = X^T X with v_mfma_f64_16x16x4_f64 (lower+upper tiles) ----
-      const int T = (k + 15) / 16;
-      const int ntiles = T * (T + 1) / 2;
-      for (int t = wave; t < ntiles; t += NR_WAVES) {
-        // tile t -> (I, J), I <= J, row-major over the upper triangle
-        int I = 0, rem = t;
-        while (rem >= T - I) { rem -= T - I; ++I; }
-        const int J = I + rem;
-        const int ci = I * 16 + (lane & 15), cj = J * 16 + (lane & 15);
-        const int kk = lane >> 4;
-        const double* coli = ci < k ? X + (int64_t)idx[ci] * S : nullptr;
-        const double* colj = cj < k ? X + (int64_t)idx[cj] * S : nullptr;
-        nr_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int s0 = 0; s0 < S; s0 += 4) {
-          const int s = s0 + kk;
-          const double a = (coli && s < S) ? coli[s] : 0.0;
-          const double b = (colj && s < S) ? colj[s] : 0.0;
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-        }
-        // D[row = (lane>>4) + 4 r][col = lane & 15]
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gi = I * 16 + (lane >> 4) + 4 * r;
-          const int gj = J * 16 + (lane & 15);
-          G[gi + (int64_t)gj * kp] = acc[r];
-          G[gj + (int64_t)gi * kp] = acc[r];
-        }
-      }
-      __syncthreads();
-
-      // ---- Lanczos with full (two-pass classical Gram-Schmidt) reorthogonalisation ----
+    if (!nonfinite) {
+      for (int c = tid; c < k; c += NR_BS) colm[c] = G[k + (int64_t)c * ld] / Sd;
+      // ---- Lanczos with full reorthogonalisation (3-term update + one CGS pass) ----
       const int mcap = k < mmax ? k : mmax;
+      double nq[1] = {0.0};
       for (int c = tid; c < k; c += NR_BS) {
         const uint32_t hsh = nr_lowbias32((uint32_t)c * 0x9E3779B9u + 0x1234567u);
-        q[c] = 1.0 + 0.01 * ((double)(hsh & 0xFFFF) / 65536.0 - 0.5);
+        const double v = 1.0 + 0.01 * ((double)(hsh & 0xFFFF) / 65536.0 - 0.5);
+        q[c] = v;
+        qprev[c] = 0.0;
+        nq[0] += v * v;
       }
-      __syncthreads();
+      block_sums<1>(nq, red);
       {
-        double a[1] = {0.0};
-        for (int c = tid; c < k; c += NR_BS) a[0] += q[c] * q[c];
-        block_sums<1>(a, red);
-        const double inv = 1.0 / sqrt(a[0]);
+        const double inv = 1.0 / sqrt(nq[0]);
         for (int c = tid; c < k; c += NR_BS) q[c] *= inv;
       }
       if (tid == 0) s_done = 0;
       __syncthreads();
       int nsteps = 0;
+      double beta_prev = 0.0;
+      // Convergence of the top Ritz pair is tested at step 16 and every 8 steps
+      // after (each test is a tridiagonal eigen-solve on one wave).
+      int next_check = mcap < 16 ? mcap : 16;
       for (int j = 0; j < mcap; ++j) {
-        // store q_j, w = G q_j
         for (int c = tid; c < k; c += NR_BS) Q[(int64_t)j * k + c] = q[c];
-        for (int r = tid; r < k; r += NR_BS) {
-          double s = 0.0;
-          for (int c = 0; c < k; ++c) s += G[r + (int64_t)c * kp] * q[c];
-          w[r] = s;
-        }
-        __syncthreads();
-        double alpha_j = 0.0;
-        for (int pass = 0; pass < 2; ++pass) {
-          // h_i = Q_i . w, i <= j  (one wave per dot)
-          for (int i = wave; i <= j; i += NR_WAVES) {
-            double s = 0.0;
-            for (int c = lane; c < k; c += 64) s += Q[(int64_t)i * k + c] * w[c];
-            s = wave_sum(s);
-            if (lane == 0) h[i] = s;
-          }
-          __syncthreads();
-          alpha_j += h[j];
-          for (int c = tid; c < k; c += NR_BS) {
-            double s = 0.0;
-            for (int i = 0; i <= j; ++i) s += h[i] * Q[(int64_t)i * k + c];
-            w[c] -= s;
-          }
-          __syncthreads();
-        }
-        double nb[1] = {0.0};
-        for (int c = tid; c < k; c += NR_BS) nb[0] += w[c] * w[c];
-        block_sums<1>(nb, red);
-        const double beta_j = sqrt(nb[0]);
+        NR_STAMP(2);  // Lanczos: vector updates / tridiagonal checks
+        const double alpha0 = matvec(G, ld, k, q, w, part, kmax, q, red);
+        NR_STAMP(3);  // Lanczos: matvec
+        const double nb = reorthogonalise(Q, k, j + 1, w, q, qprev, alpha0, beta_prev, h, red);
+        NR_STAMP(4);  // Lanczos: reorthogonalisation
+        const double alpha_j = alpha0 + h[j];
+        const double beta_j = sqrt(nb);
         if (tid == 0) {
           alpha[j] = alpha_j;
           beta[j] = beta_j;
@@ -487,46 +650,50 @@ module_profile_kernel(ProfileParams P) {
         nsteps = j + 1;
         __syncthreads();
         const bool last = (j + 1 == mcap);
-        if (((j + 1) % 4 == 0) || last || beta_j <= 1e-300) {
+        if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
+          next_check += 8;
           if (wave == 0) {
             const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane);
             if (lane == 0) {
               tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
               const double resid = beta_j * fabs(ty[j]);
-              s_done = (resid <= 5e-15 * fabs(theta)) || last || beta_j <= 1e-300 * fabs(theta) ||
-                        beta_j == 0.0;
-              if (last && !(resid <= 5e-15 * fabs(theta)) && P.diag) atomicAdd(P.diag, 1);
+              const bool conv = resid <= 5e-15 * fabs(theta);
+              s_done = conv || last || !(beta_j > 1e-300 * fabs(theta));
+              if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
             }
           }
           __syncthreads();
           if (s_done) break;
         }
         const double inv = 1.0 / beta_j;
-        for (int c = tid; c < k; c += NR_BS) q[c] = w[c] * inv;
+        for (int c = tid; c < k; c += NR_BS) {
+          qprev[c] = q[c];
+          q[c] = w[c] * inv;
+        }
+        beta_prev = beta_j;
         __syncthreads();
       }
-      // Ritz vector v = Q y, then G v
+      NR_STAMP(2);
+      if (tid == 0 && P.diag) {
+        atomicAdd(P.diag + 1, 1);
+        atomicAdd(P.diag + 2, nsteps);
+      }
+      // Ritz vector v = Q y, normalised, then G v
+      double nv[1] = {0.0};
       for (int c = tid; c < k; c += NR_BS) {
         double s = 0.0;
         for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
         vv[c] = s;
+        nv[0] += s * s;
       }
-      __syncthreads();
+      block_sums<1>(nv, red);
       {
-        double a[1] = {0.0};
-        for (int c = tid; c < k; c += NR_BS) a[0] += vv[c] * vv[c];
-        block_sums<1>(a, red);
-        const double inv = 1.0 / sqrt(a[0]);
+        const double inv = 1.0 / sqrt(nv[0]);
         for (int c = tid; c < k; c += NR_BS) vv[c] *= inv;
       }
       __syncthreads();
-      for (int r = tid; r < k; r += NR_BS) {
-        double s = 0.0;
-        for (int c = 0; c < k; ++c) s += G[r + (int64_t)c * kp] * vv[c];
-        gv[r] = s;
-      }
-      __syncthreads();
-      // lambda = v.Gv, ubar = sum_j m_j v_j / sigma
+      matvec(G, ld, k, vv, gv, part, kmax, nullptr, red);
+      // lambda = v.Gv; ubar = mean of u = X v / sigma
       double a3[2] = {0.0, 0.0};
       for (int c = tid; c < k; c += NR_BS) {
         a3[0] += vv[c] * gv[c];
@@ -536,22 +703,22 @@ module_profile_kernel(ProfileParams P) {
       const double lambda = a3[0];
       const double sigma = sqrt(lambda);
       const double ubar = a3[1] / sigma;
-      const double Sd = (double)S;
       const double var_u = 1.0 - Sd * ubar * ubar;  // sum (u - ubar)^2 with |u| = 1
-      // orientation: sign(cor(meanObs, u)) (src/netStats.cpp:242-247)
-      double a4[3] = {0.0, 0.0, 0.0};
-      for (int c = tid; c < k; c += NR_BS) a4[0] += gv[c] / sigma - Sd * colm[c] * ubar;
-      for (int r = tid; r < S; r += NR_BS) a4[1] += mo[r];
-      block_sums<3>(a4, red);
-      const double mo_mean = a4[1] / Sd;
-      double a5[1] = {0.0};
-      for (int r = tid; r < S; r += NR_BS) a5[0] += (mo[r] - mo_mean) * (mo[r] - mo_mean);
-      block_sums<1>(a5, red);
-      const bool flip = (a4[0] < 0.0) && (a5[0] > 0.0) && (var_u > 0.0);
-      const double sgn = flip ? -1.0 : 1.0;
-      // NC_j = cor(x_j, u) (src/netStats.cpp:279), node order = CSR order
+      // orientation: sign(cor(meanObs, u)) (src/netStats.cpp:242-247); the sign
+      // of the covariance is that of sum_j cov(x_j, u); var(meanObs) * k^2 * (S-1)
+      // = 1'G1 - (sum of all data)^2 / S.
+      double a4[2] = {0.0, 0.0};
       for (int c = tid; c < k; c += NR_BS) {
-        const double gjj = G[c + (int64_t)c * kp];
+        a4[0] += gv[c] / sigma - Sd * colm[c] * ubar;
+        a4[1] += colm[c];
+      }
+      block_sums<2>(a4, red);
+      const double var_mo = ones_g_ones - Sd * a4[1] * a4[1];
+      const bool flip = (a4[0] < 0.0) && (var_mo > 0.0) && (var_u > 0.0);
+      const double sgn = flip ? -1.0 : 1.0;
+      // NC_j = cor(x_j, u) (src/netStats.cpp:279); node order = CSR order
+      for (int c = tid; c < k; c += NR_BS) {
+        const double gjj = G[c + (int64_t)c * ld];
         const double cov = gv[c] / sigma - Sd * colm[c] * ubar;
         const double var_x = gjj - Sd * colm[c] * colm[c];
         w[c] = sgn * cov / (sqrt(var_x) * sqrt(var_u));
@@ -584,7 +751,8 @@ module_profile_kernel(ProfileParams P) {
       if (P.nc_out) P.nc_out[off + c] = y;
     }
     block_sums<5>(b1, red);
-    stat_coh = b1[0] >= 1.0 ? b1[1] / b1[0] : nr_nan();
+    const double stat_coh = b1[0] >= 1.0 ? b1[1] / b1[0] : nr_nan();
+    double stat_cc = nr_nan(), stat_ac = nr_nan();
     if (P.disc_nc && P.out) {
       const double mx = b1[3] / b1[2], my = b1[4] / b1[2];
       double b2[4] = {0, 0, 0, 0};
@@ -612,6 +780,7 @@ module_profile_kernel(ProfileParams P) {
       if (P.coh_out) P.coh_out[m] = stat_coh;
     }
     __syncthreads();
+    NR_STAMP(5);  // Ritz vector, contributions, statistics
   }
 }
 
@@ -701,10 +870,13 @@ __global__ void export_indices_kernel(IndexSource src, int64_t n_nodes_total, in
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-size_t net_kernel_lds(int k_max) { return sizeof(double) * (8 * NR_WAVES + k_max) + sizeof(uint32_t) * k_max; }
+size_t net_kernel_lds(int k_max) {
+  return sizeof(double) * (8 * NR_WAVES + (size_t)NR_WAVES * k_max) + sizeof(uint32_t) * k_max;
+}
 
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples) {
-  return sizeof(double) * (8 * NR_WAVES + 5 * (size_t)k_max + n_samples + 9 * (size_t)m_max) +
+  (void)n_samples;
+  return sizeof(double) * (8 * NR_WAVES + (6 + NR_WAVES) * (size_t)k_max + 9 * (size_t)m_max) +
          sizeof(uint32_t) * k_max;
 }
 

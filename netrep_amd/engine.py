@@ -197,6 +197,20 @@ class Engine:
                                             C.byref(items)))
         return ms.value, launches.value, items.value
 
+    def diagnostics(self):
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        self._check(self._lib.nr_get_diagnostics(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"eig_items": a.value, "eig_steps": b.value, "eig_cap_hits": c.value}
+
+    def set_stamps(self, enable: bool):
+        self._check(self._lib.nr_set_stamps(self._h, int(bool(enable))))
+
+    def stamps(self):
+        out = (C.c_uint64 * 8)()
+        self._check(self._lib.nr_get_stamps(self._h, out))
+        names = ["index", "gram", "lanczos_vec", "lanczos_matvec", "reorth", "tail"]
+        return dict(zip(names, list(out)[:6]))
+
     def reset_timing(self):
         self._check(self._lib.nr_reset_timing(self._h))
 

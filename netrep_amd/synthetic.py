@@ -73,6 +73,7 @@ def numpy_dataset(layout: Layout, n_samples: int, seed: int, preserve_all: bool 
     preserved = set(mods) if preserve_all else set(mods[::2])
     x = _gen_numpy(layout, n_samples, rng, preserved)
     corr = np.corrcoef(x, rowvar=False)
+    corr = np.triu(corr) + np.triu(corr, 1).T     # exactly symmetric, as R's cor() returns
     net = np.abs(corr) ** 5
     return x, corr, net
 
@@ -99,7 +100,8 @@ def torch_dataset(layout: Layout, n_samples: int, seed: int, preserve_all: bool 
         xt[p] = r[:, None] * e[None, :] + torch.sqrt(1 - r * r)[:, None] * xt[p]
     xc = xt - xt.mean(dim=1, keepdim=True)
     xc = xc / xc.norm(dim=1, keepdim=True)
-    corr = xc @ xc.T            # symmetric: row-major == column-major
+    corr = xc @ xc.T
+    corr = torch.triu(corr) + torch.triu(corr, 1).T   # bitwise symmetric, as R's cor() returns
     corr.diagonal().fill_(1.0)
     net = corr.abs().pow(5)
     return xt, corr, net
