@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 import netrep_amd as N  # noqa: E402
 from netrep_amd import synthetic as S  # noqa: E402
+from netrep_amd.distributed import broadcast_tensors, gather_nulls, perm_range  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TFS = 78.6    # MI355X fp64 matrix peak (spec)
@@ -37,11 +38,12 @@ FP64_MFMA_PEAK_TFS = 78.6    # MI355X fp64 matrix peak (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=256, help="permutations per step")
     ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4"])
-    ap.add_argument("--cpu-baseline-perms", type=int, default=4)
+    ap.add_argument("--cpu-baseline-perms", type=int, default=0,
+                    help="CPU sample size (0: sized for ~15 s on the host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--stamps", action="store_true",
@@ -108,8 +110,7 @@ def build_case(cfg, world, rank, local, seed):
     if world > 1:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for t in (tc, tn, txs):
-            dist.broadcast(t, src=0)
+        broadcast_tensors([tc, tn, txs], src=0)   # RCCL over xGMI
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - t0
     eng.set_dataset_device(tc.data_ptr(), tn.data_ptr(), txs.data_ptr() if with_data else 0,
@@ -138,31 +139,30 @@ def roofline_terms(sizes, n_samples, with_data):
 
 
 def cpu_baseline(lay, meta, host, n_perm, seed):
-    """Oracle (numpy/scipy restatement of the reference's CPU path) on a bounded
-    sample of the same workload, single thread."""
-    sys.path.insert(0, ROOT)
-    from oracle import netrep_oracle as O
-    from oracle import prp
+    """The C++ CPU restatement of the reference's path (oracle/netrep_ref.cpp:
+    per-thread contiguous permutation chunks, one null-pool shuffle per
+    permutation, LAPACK dgesdd per module) on a bounded sample of the same
+    workload, using the host cores of this GPU's share (at most 16)."""
+    from oracle import ref_cpp
+    threads = max(1, min(16, os.cpu_count() or 1))
     tc = host["tc"].cpu().numpy()
     tn = host["tn"].cpu().numpy()
-    tx = host["txs"].cpu().numpy().T.copy()  # S x N
-    mods = lay.modules
-    mi = O.ModuleIndex(lay.names, lay.labels, lay.names, mods)
+    tx = host["txs"].cpu().numpy().T if meta["with_data"] else None   # S x N view, column-major
     no = meta["node_off"]
-    disc = {"corr": {}, "degree": {}, "contribution": {}}
-    cvo = 0
-    for j, m in enumerate(mods):
-        kk = int(no[j + 1] - no[j])
-        disc["corr"][m] = meta["disc_cv"][cvo:cvo + kk * (kk - 1) // 2]
-        disc["degree"][m] = meta["disc_wd"][no[j]:no[j + 1]]
-        disc["contribution"][m] = meta["disc_nc"][no[j]:no[j + 1]]
-        cvo += kk * (kk - 1) // 2
-    nn = mi.null_idx.size
-    pis = np.stack([prp.permute(np.arange(nn), nn, seed, p) for p in range(n_perm)]).astype(np.int64)
+    args = dict(n_rows=len(lay.modules), row_of=np.arange(len(lay.modules)), node_off=no,
+                test_idx=meta["idx"], null_pos=meta["idx"], null_idx=np.arange(meta["n_nodes"]),
+                disc_cv=meta["disc_cv"], disc_wd=meta["disc_wd"],
+                disc_nc=meta["disc_nc"] if meta["with_data"] else None, seed=seed, n_threads=threads,
+                want_observed=False)
+    if n_perm <= 0:   # size the sample for ~15 s of CPU work
+        t0 = time.perf_counter()
+        ref_cpp.permutation_procedure(tx, tc, tn, n_perm=threads, **args)
+        rate = threads / max(time.perf_counter() - t0, 1e-9)      # permutations/s, all threads
+        n_perm = int(max(threads, min(100000, 15.0 * rate)))
     t0 = time.perf_counter()
-    O.permutation_procedure(disc, tx, tc, tn, mi, pis, with_data=meta["with_data"])
+    ref_cpp.permutation_procedure(tx, tc, tn, n_perm=n_perm, **args)
     dt = time.perf_counter() - t0
-    return n_perm / dt, dt
+    return n_perm / dt, dt, n_perm, threads
 
 
 def main():
@@ -177,7 +177,7 @@ def main():
         p0 = base + s * B
         return eng.run(p0, p0 + B, args.seed)
 
-    base_w = 10**9 + rank * W * B
+    base_w = 10**12 + rank * W * B        # warm-up permutations, outside the measured range
     for s in range(W):
         step(s, base_w)
     eng.synchronize()
@@ -189,9 +189,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    base = rank * K * B
+    total_perms = world * K * B
+    base, _ = perm_range(rank, world, total_perms)   # this rank's contiguous chunk
+    chunks = []
     for s in range(K):
-        nulls = step(s, base)
+        chunks.append(step(s, base))
     eng.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -203,13 +205,14 @@ def main():
         elapsed = float(t.item())
     ms0, l0, _ = eng.timing(0)
     ms1, l1, _ = eng.timing(1)
-    finite = float(np.isfinite(nulls).mean())
+    local = np.concatenate(chunks, axis=2)
+    cube = gather_nulls(local, rank, world, total_perms) if world > 1 else local
+    finite = float(np.isfinite(cube).mean()) if rank == 0 else None
     diag = eng.diagnostics()
     if args.stamps:
         diag["stamps_cycles"] = eng.stamps()
 
     if rank == 0:
-        total_perms = world * K * B
         value = total_perms / elapsed
         # dominant kernel + roofline (per launch = one batch of B permutations)
         kernels = {
@@ -231,10 +234,11 @@ def main():
                     "traffic": None}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and host is not None:
-            rate, dt = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)
-            cpu = {"value": rate, "unit": "permutations/sec", "cores": 1, "kind": "port",
-                   "sample": f"{args.cpu_baseline_perms} permutations x 50 modules of the same workload, "
-                             f"numpy/scipy restatement (gesdd SVD), {dt:.1f} s"}
+            rate, dt, n_cpu, threads = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)
+            cpu = {"value": rate, "unit": "permutations/sec", "cores": threads, "kind": "port",
+                   "sample": f"{n_cpu} permutations x {len(lay.modules)} modules of the same workload in "
+                             f"{dt:.1f} s: C++ restatement of src/permutations.cpp (std::thread chunks, "
+                             f"LAPACK dgesdd), {threads} threads"}
         line = {
             "metric": "permutations/sec (whole node), 20k genes x 50 modules",
             "value": value,
