@@ -153,9 +153,10 @@ int nr_get_timing(nr_ctx* ctx, int kernel, double* total_ms, int64_t* launches,
                   int64_t* items);
 int nr_reset_timing(nr_ctx* ctx);
 /* Summary-profile eigen-solver counters since the last nr_reset_timing:
- * items solved, Lanczos steps taken, items that reached the step cap. */
+ * items solved, Lanczos steps taken, items that reached the step cap, and
+ * partial-reorthogonalisation passes performed. */
 int nr_get_diagnostics(nr_ctx* ctx, int64_t* eig_items, int64_t* eig_steps,
-                       int64_t* eig_cap_hits);
+                       int64_t* eig_cap_hits, int64_t* eig_reorths);
 int nr_synchronize(nr_ctx* ctx);
 /* Diagnostics: per-phase shader-cycle stamps of the summary-profile kernel,
  * summed over workgroups (0 index, 1 Gram, 2 Lanczos vector work, 3 Lanczos

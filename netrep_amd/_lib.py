@@ -75,7 +75,7 @@ SIGNATURES = {
     "nr_set_timing": (_int, [_p, _int]),
     "nr_get_timing": (_int, [_p, _int, _dp, _i64p, _i64p]),
     "nr_reset_timing": (_int, [_p]),
-    "nr_get_diagnostics": (_int, [_p, _i64p, _i64p, _i64p]),
+    "nr_get_diagnostics": (_int, [_p, _i64p, _i64p, _i64p, _i64p]),
     "nr_synchronize": (_int, [_p]),
     "nr_set_stamps": (_int, [_p, _int]),
     "nr_get_stamps": (_int, [_p, C.POINTER(C.c_uint64)]),

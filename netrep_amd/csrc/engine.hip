@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -73,7 +74,7 @@ struct nr_ctx {
   size_t pi_cap = 0;
   double* d_scratch = nullptr;
   size_t scratch_cap = 0;
-  int* d_counters = nullptr;  // [0] queue head, [1..3] lanczos diagnostics, [4] flag
+  int* d_counters = nullptr;  // [0] queue head, [1..4] lanczos diagnostics, [5] flag
   int64_t batch = 0;          // 0 = automatic
 
   std::atomic<int64_t> done{0}, total{0};
@@ -158,25 +159,46 @@ int profile_m_max(int k_max) { return std::min(k_max, 160); }
 // padded to a 32-column super-tile.
 int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
 
-// Persistent profile workgroups: as many per CU as LDS allows (at most 4).
-int profile_slots(const nr_ctx* ctx, int64_t n_items, int k_max, int n_samples) {
+// Launch plan of the summary-profile kernel. Default: the full-Gram variant
+// (4-wave workgroups, 3 per CU), measured fastest at C3. The packed variant
+// (8-wave workgroups, packed symmetric Gram, half the Lanczos bytes) is kept
+// for A/B measurement: NETREP_PROFILE_VARIANT=packed (NETREP_PACKED_WG_PER_CU).
+struct ProfilePlan {
+  bool packed = false;
+  int slots = 0;
+  int per_cu = 1;
+  int64_t gram_doubles = 0, stride = 0;
+};
+
+int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, ProfilePlan* plan) {
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-  const size_t lds = nr::profile_kernel_lds(k_max, profile_m_max(k_max), n_samples);
-  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / lds));
-  const int64_t slots = std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu);
-  return (int)std::max<int64_t>(slots, 1);
-}
-
-bool profile_fits(int k_max, int n_samples) {
-  return nr::profile_kernel_lds(k_max, profile_m_max(k_max), n_samples) <= 160 * 1024;
-}
-
-int ensure_scratch(nr_ctx* ctx, int slots, int k_max, int64_t* stride_out) {
-  const int64_t ld = gram_ld(k_max);
-  const int64_t stride = ld * ld + (int64_t)k_max * profile_m_max(k_max);
-  *stride_out = stride;
-  return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(stride * slots));
+  const int m = profile_m_max(k_max);
+  const size_t lds_packed = nr::profile_kernel_lds(k_max, m, n_samples, true);
+  const size_t lds_full = nr::profile_kernel_lds(k_max, m, n_samples, false);
+  const char* force = std::getenv("NETREP_PROFILE_VARIANT");
+  bool packed = false;
+  if (force && std::string(force) == "full") packed = false;
+  if (force && std::string(force) == "packed" && lds_packed <= 160 * 1024) packed = true;
+  const size_t lds = packed ? lds_packed : lds_full;
+  if (lds > 160 * 1024)
+    return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
+  int want = packed ? 2 : 3;
+  if (const char* e = std::getenv("NETREP_PACKED_WG_PER_CU"))
+    if (packed) want = std::max(1, std::min(2, std::atoi(e)));
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
+  plan->packed = packed;
+  plan->per_cu = per_cu;
+  plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu));
+  if (packed) {
+    const int64_t kc = k_max + 1;
+    plan->gram_doubles = (kc * (kc + 1) / 2 + 31) / 32 * 32;
+  } else {
+    const int64_t ld = gram_ld(k_max);
+    plan->gram_doubles = ld * ld;
+  }
+  plan->stride = plan->gram_doubles + (int64_t)k_max * m;
+  return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
 }
 
 void timer_begin(nr_ctx* ctx, int which) {
@@ -246,11 +268,8 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   timer_end(ctx, 0, n_items);
 
   if (data) {
-    if (!profile_fits(ctx->k_max, (int)ctx->n_samples))
-      return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
-    const int slots = profile_slots(ctx, n_items, ctx->k_max, (int)ctx->n_samples);
-    int64_t stride = 0;
-    rc = ensure_scratch(ctx, slots, ctx->k_max, &stride);
+    ProfilePlan plan;
+    rc = plan_profile(ctx, n_items, ctx->k_max, (int)ctx->n_samples, &plan);
     if (rc) return rc;
     NR_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream));
     nr::ProfileParams pp{};
@@ -264,6 +283,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.n_items = (int32_t)n_items;
     pp.k_max = ctx->k_max;
     pp.ld = gram_ld(ctx->k_max);
+    pp.gram_doubles = plan.gram_doubles;
     pp.m_max = profile_m_max(ctx->k_max);
     pp.row_of = ctx->d_row_of;
     pp.n_rows = ctx->n_rows;
@@ -273,12 +293,12 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.slot_avg_contrib = 6;
     pp.out = d_out;
     pp.scratch = ctx->d_scratch;
-    pp.scratch_stride = stride;
+    pp.scratch_stride = plan.stride;
     pp.queue = ctx->d_counters;
     pp.diag = ctx->d_counters + 1;
     pp.stamps = ctx->d_stamps;
     timer_begin(ctx, 1);
-    NR_HIP(ctx, nr::launch_profile(pp, slots, ctx->stream));
+    NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.packed, plan.per_cu, ctx->stream));
     timer_end(ctx, 1, n_items);
   }
   return NR_OK;
@@ -467,10 +487,10 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
     (void)hipFree(tn);
     if (e != hipSuccess) return hip_fail(ctx, e, "dataset upload");
   }
-  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 4, 0, sizeof(int), ctx->stream));
-  NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 4, ctx->stream));
+  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream));
+  NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 5, ctx->stream));
   int asym = 0;
-  NR_HIP(ctx, hipMemcpyAsync(&asym, ctx->d_counters + 4, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  NR_HIP(ctx, hipMemcpyAsync(&asym, ctx->d_counters + 5, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   if (data) {
     const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
     NR_HIP(ctx, hipMalloc((void**)&ctx->d_data, bytes));
@@ -682,13 +702,8 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
     np.avgw_out = d_aw;
     e = nr::launch_net(np, n_mod, ctx->stream);
     if (e == hipSuccess && ctx->d_data && (contribution || summary || coherence)) {
-      if (!profile_fits(kmax, (int)S)) {
-        rc = fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
-        break;
-      }
-      const int slots = profile_slots(ctx, n_mod, kmax, (int)S);
-      int64_t stride = 0;
-      if ((rc = ensure_scratch(ctx, slots, kmax, &stride))) break;
+      ProfilePlan plan;
+      if ((rc = plan_profile(ctx, n_mod, kmax, (int)S, &plan))) break;
       e = hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream);
       nr::ProfileParams pp{};
       pp.data = ctx->d_data;
@@ -700,15 +715,16 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
       pp.n_items = n_mod;
       pp.k_max = kmax;
       pp.ld = gram_ld(kmax);
+      pp.gram_doubles = plan.gram_doubles;
       pp.m_max = profile_m_max(kmax);
       pp.sp_out = d_sp;
       pp.nc_out = d_nc;
       pp.coh_out = d_coh;
       pp.scratch = ctx->d_scratch;
-      pp.scratch_stride = stride;
+      pp.scratch_stride = plan.stride;
       pp.queue = ctx->d_counters;
       pp.diag = ctx->d_counters + 1;
-      if (e == hipSuccess) e = nr::launch_profile(pp, slots, ctx->stream);
+      if (e == hipSuccess) e = nr::launch_profile(pp, plan.slots, plan.packed, plan.per_cu, ctx->stream);
     }
     auto d2h = [&](double* h, const double* d, int64_t n) {
       if (e == hipSuccess && h && n > 0)
@@ -752,15 +768,15 @@ int nr_check_finite(nr_ctx* ctx, const double* mat, int64_t n_elem, int* all_fin
   const int64_t chunk = std::min<int64_t>(n_elem, (int64_t)1 << 26);
   double* d = nullptr;
   NR_HIP(ctx, hipMalloc((void**)&d, (size_t)chunk * sizeof(double)));
-  hipError_t e = hipMemsetAsync(ctx->d_counters + 4, 0, sizeof(int), ctx->stream);
+  hipError_t e = hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream);
   for (int64_t o = 0; o < n_elem && e == hipSuccess; o += chunk) {
     const int64_t len = std::min(chunk, n_elem - o);
     e = hipMemcpyAsync(d, mat + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = nr::launch_finite(d, len, ctx->d_counters + 4, ctx->stream);
+    if (e == hipSuccess) e = nr::launch_finite(d, len, ctx->d_counters + 5, ctx->stream);
   }
   int bad = 0;
   if (e == hipSuccess)
-    e = hipMemcpyAsync(&bad, ctx->d_counters + 4, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    e = hipMemcpyAsync(&bad, ctx->d_counters + 5, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   (void)hipFree(d);
   if (e != hipSuccess) return hip_fail(ctx, e, "check finite");
@@ -806,7 +822,7 @@ int nr_reset_timing(nr_ctx* ctx) {
   ctx->timers[0] = DeviceTimer();
   ctx->timers[1] = DeviceTimer();
   NR_HIP(ctx, hipSetDevice(ctx->device));
-  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 1, 0, 3 * sizeof(int), ctx->stream));
+  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 1, 0, 4 * sizeof(int), ctx->stream));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return NR_OK;
 }
@@ -830,15 +846,17 @@ int nr_get_stamps(nr_ctx* ctx, uint64_t* cycles) {
   return NR_OK;
 }
 
-int nr_get_diagnostics(nr_ctx* ctx, int64_t* eig_items, int64_t* eig_steps, int64_t* eig_cap_hits) {
+int nr_get_diagnostics(nr_ctx* ctx, int64_t* eig_items, int64_t* eig_steps, int64_t* eig_cap_hits,
+                       int64_t* eig_reorths) {
   if (!ctx) return NR_ERR_INVALID;
-  int h[3] = {0, 0, 0};
+  int h[4] = {0, 0, 0, 0};
   NR_HIP(ctx, hipSetDevice(ctx->device));
-  NR_HIP(ctx, hipMemcpyAsync(h, ctx->d_counters + 1, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  NR_HIP(ctx, hipMemcpyAsync(h, ctx->d_counters + 1, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (eig_cap_hits) *eig_cap_hits = h[0];
   if (eig_items) *eig_items = h[1];
   if (eig_steps) *eig_steps = h[2];
+  if (eig_reorths) *eig_reorths = h[3];
   return NR_OK;
 }
 

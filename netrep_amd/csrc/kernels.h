@@ -51,7 +51,8 @@ struct ProfileParams {
   int32_t n_perm;
   int32_t n_items;
   int32_t k_max, m_max;
-  int32_t ld;                  // leading dimension of the per-slot Gram
+  int32_t ld;                  // leading dimension of the per-slot Gram (full storage)
+  int64_t gram_doubles;        // doubles reserved for the Gram per slot
   const int32_t* row_of;
   int32_t n_rows, n_stat;
   int32_t slot_coherence, slot_cor_contrib, slot_avg_contrib;
@@ -62,14 +63,15 @@ struct ProfileParams {
   double* scratch;             // per-slot Gram (ld x ld) + Lanczos basis (k_max x m_max)
   int64_t scratch_stride;
   int* queue;                  // work-queue head, zeroed before launch
-  int* diag;                   // [0] Lanczos step-cap hits, [1] items, [2] Lanczos steps
+  int* diag;                   // [0] Lanczos step-cap hits, [1] items, [2] Lanczos steps, [3] reorthogonalisations
   unsigned long long* stamps;  // [8] per-phase shader cycles (diagnostics; NULL = off)
 };
 
 size_t net_kernel_lds(int k_max);
-size_t profile_kernel_lds(int k_max, int m_max, int n_samples);
+size_t profile_kernel_lds(int k_max, int m_max, int n_samples, bool packed);
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
-hipError_t launch_profile(const ProfileParams& P, int n_slots, hipStream_t st);
+hipError_t launch_profile(const ProfileParams& P, int n_slots, bool packed, int wg_per_cu,
+                          hipStream_t st);
 hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,
                              hipStream_t st);
 hipError_t launch_symmetry(const double2* a, int64_t n, int* asym, hipStream_t st);

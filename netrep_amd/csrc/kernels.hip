@@ -38,21 +38,21 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // Block-wide sums of N values; result broadcast to every thread. `red` must
 // hold N * NR_WAVES doubles of LDS. Contains two barriers.
-template <int N>
+template <int N, int NW = NR_WAVES>
 __device__ __forceinline__ void block_sums(double (&v)[N], double* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
   if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) red[i * NR_WAVES + wave] = v[i];
+    for (int i = 0; i < N; ++i) red[i * NW + wave] = v[i];
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < NR_WAVES; ++w) s += red[i * NR_WAVES + w];
+    for (int w = 0; w < NW; ++w) s += red[i * NW + w];
     v[i] = s;
   }
   __syncthreads();
@@ -410,17 +410,27 @@ __device__ __forceinline__ double matvec(const double* __restrict__ G, int ld, i
   return d[0];
 }
 
-// Lanczos reorthogonalisation against the stored basis Q (column-major k x n)
-// of the 3-term-corrected vector z = w - a q - b qprev: z is formed in LDS
-// once, h = Q^T z with four dots in flight per wave, then w <- z - Q h.
-// Returns |w|^2.
+// Lanczos 3-term step w <- w - a q - b qprev; returns |w|^2.
+template <int NW = NR_WAVES>
+__device__ __forceinline__ double three_term(int k, double* w, const double* q, const double* qprev,
+                                             double a, double b, double* red) {
+  double nrm[1] = {0.0};
+  for (int c = threadIdx.x; c < k; c += NW * 64) {
+    const double z = w[c] - a * q[c] - b * qprev[c];
+    w[c] = z;
+    nrm[0] += z * z;
+  }
+  block_sums<1, NW>(nrm, red);
+  return nrm[0];
+}
+
+// Classical Gram-Schmidt of w against the stored basis Q (column-major k x n):
+// h = Q^T w (four dots in flight per wave), w <- w - Q h. Returns |w|^2.
+template <int NW = NR_WAVES>
 __device__ __forceinline__ double reorthogonalise(const double* __restrict__ Q, int k, int n, double* w,
-                                                  const double* q, const double* qprev, double a,
-                                                  double b, double* h, double* red) {
+                                                  double* h, double* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = threadIdx.x; c < k; c += NR_BS) w[c] = w[c] - a * q[c] - b * qprev[c];
-  __syncthreads();
-  for (int i0 = 4 * wave; i0 < n; i0 += 4 * NR_WAVES) {
+  for (int i0 = 4 * wave; i0 < n; i0 += 4 * NW) {
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     for (int c = lane; c < k; c += 64) {
       const double z = w[c];
@@ -436,7 +446,7 @@ __device__ __forceinline__ double reorthogonalise(const double* __restrict__ Q, 
   }
   __syncthreads();
   double nrm[1] = {0.0};
-  for (int c = threadIdx.x; c < k; c += NR_BS) {
+  for (int c = threadIdx.x; c < k; c += NW * 64) {
     double acc = 0.0;
     int i = 0;
     for (; i + 4 <= n; i += 4) {
@@ -449,9 +459,45 @@ __device__ __forceinline__ double reorthogonalise(const double* __restrict__ Q, 
     w[c] = z;
     nrm[0] += z * z;
   }
-  block_sums<1>(nrm, red);
+  block_sums<1, NW>(nrm, red);
   return nrm[0];
 }
+
+// Partial reorthogonalisation (Simon 1984): omega_{j+1,i} estimates q_{j+1}.q_i
+// from the recurrence on T's entries; run by one wave over i = 0..j. Returns
+// max_i |omega_{j+1,i}| (all lanes). om_cur = omega_{j,.}, om_prev = omega_{j-1,.}.
+__device__ __forceinline__ double omega_update(const double* alpha, const double* beta, int j, double beta_j,
+                                               const double* om_cur, const double* om_prev, double* om_next,
+                                               double anorm, int k, int lane) {
+  const double eps = 2.220446049250313e-16;
+  const double psi = eps * anorm / beta_j;
+  double mx = 0.0;
+  for (int i = lane; i < j; i += 64) {
+    double t = beta[i] * om_cur[i + 1] + (alpha[i] - alpha[j]) * om_cur[i] -
+               (j > 0 ? beta[j - 1] * om_prev[i] : 0.0);
+    if (i > 0) t += beta[i - 1] * om_cur[i - 1];
+    t = t / beta_j;
+    t += t >= 0.0 ? psi : -psi;
+    om_next[i] = t;
+    mx = fmax(mx, fabs(t));
+  }
+  if (lane == 0) {
+    om_next[j] = eps * sqrt((double)k) * anorm / beta_j;
+    om_next[j + 1] = 1.0;
+    mx = fmax(mx, fabs(om_next[j]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+  return mx;
+}
+
+// Packed symmetric storage: lower triangle, column-major, over kc = k + 1
+// columns (the last is the virtual all-ones column); column c holds rows
+// c .. kc-1 from pk_col(c, kc).
+__device__ __forceinline__ int64_t pk_col(int c, int kc) {
+  return (int64_t)c * kc - (int64_t)c * (c - 1) / 2;
+}
+__device__ __forceinline__ int64_t pk_at(int r, int c, int kc) { return pk_col(c, kc) + (r - c); }
 
 // Loads one 4-row group of an operand column for the Gram MFMA: rows
 // s .. s+3 of a data column, of the virtual all-ones column, or zeros.
@@ -471,6 +517,7 @@ __device__ __forceinline__ void load4(const double* __restrict__ col, bool ones,
 // step (the K order of the dot products is permuted, identically for both
 // operands). Returns per-lane partial of 1^T G 1 over the X block and a
 // non-finite flag.
+template <int NW = NR_WAVES, bool PACKED = false>
 __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* idx, int k,
                           double* __restrict__ G, int ld, double& g1sum, int& bad) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -478,7 +525,7 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
   const int kc = k + 1;
   const int T2 = (kc + 31) / 32;
   const int nsup = T2 * (T2 + 1) / 2;
-  for (int t = wave; t < nsup; t += NR_WAVES) {
+  for (int t = wave; t < nsup; t += NW) {
     int I2 = 0, rem = t;
     while (rem >= T2 - I2) { rem -= T2 - I2; ++I2; }
     const int J2 = I2 + rem;
@@ -495,28 +542,48 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
-    double cur[4][4], nxt[4][4];
+    double cur[4][4];
+    if (PACKED) {
+      // register-lean: no software prefetch (two 8-wave workgroups per CU hide latency)
+      for (int s0 = 0; s0 < S; s0 += 16) {
 #pragma unroll
-    for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], 4 * kk, S, cur[o]);
-    for (int s0 = 0; s0 < S; s0 += 16) {
-      const int sn = s0 + 16 + 4 * kk;
+        for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], s0 + 4 * kk, S, cur[o]);
 #pragma unroll
-      for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], sn, S, nxt[o]);
+        for (int o = 0; o < 4; ++o)
 #pragma unroll
-      for (int o = 0; o < 4; ++o)
+          for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[2][q], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[3][q], acc[1][1], 0, 0, 0);
+        for (int q = 0; q < 4; ++q) {
+          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[2][q], acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[3][q], acc[1][1], 0, 0, 0);
+        }
       }
+    } else {
+      double nxt[4][4];
 #pragma unroll
-      for (int o = 0; o < 4; ++o)
+      for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], 4 * kk, S, cur[o]);
+      for (int s0 = 0; s0 < S; s0 += 16) {
+        const int sn = s0 + 16 + 4 * kk;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+        for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], sn, S, nxt[o]);
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[2][q], acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[3][q], acc[1][1], 0, 0, 0);
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+      }
     }
     const double wgt = (I2 == J2) ? 1.0 : 2.0;
 #pragma unroll
@@ -529,8 +596,12 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
           const int gi = I2 * 32 + 16 * a + kk + 4 * r;
           const int gj = J2 * 32 + 16 * b + i16;
           const double val = acc[a][b][r];
-          G[gi + (int64_t)gj * ld] = val;
-          G[gj + (int64_t)gi * ld] = val;
+          if (PACKED) {
+            if (gi <= gj && gj < kc) G[pk_at(gj, gi, kc)] = val;  // lower triangle, column gi
+          } else {
+            G[gi + (int64_t)gj * ld] = val;
+            G[gj + (int64_t)gi * ld] = val;
+          }
           if (gi < k && gj < k) g1sum += wgt * val;
         }
   }
@@ -549,33 +620,116 @@ __device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memti
     }                                                                           \
   } while (0)
 
-__global__ void __launch_bounds__(NR_BS, 3)
-module_profile_kernel(ProfileParams P) {
+// w = G x over the leading k x k block of the PACKED symmetric G (pk_at), NW
+// waves. Work units are (64-row block, 8-column group) pairs with columns
+// c <= last row of the block; lanes own rows. One coalesced read of each
+// column segment feeds the lower part (w_r += G_rc x_c, lane-local) and the
+// mirrored upper part (w_c += sum_{r>c} G_rc x_r), the latter reduced for 8
+// columns at once by a transpose-reduce butterfly (10 shuffles). Per-wave
+// partial arrays keep the sums deterministic. Returns sum_r y_r out_r if y.
+template <int NW>
+__device__ __forceinline__ double packed_matvec(const double* __restrict__ P, int kc, int k,
+                                                const double* x, double* out, double* part,
+                                                double* upper, int ks, const double* y, double* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < NW * ks; i += NW * 64) {
+    part[i] = 0.0;
+    upper[i] = 0.0;
+  }
+  __syncthreads();
+  const int nrb = (k + 63) / 64;
+  for (int rbi = 0; rbi < nrb; ++rbi) {
+    const int r = rbi * 64 + lane;
+    const int cmax = min(k, (rbi + 1) * 64);
+    const int ncg = (cmax + 7) / 8;
+    const double xr = r < k ? x[r] : 0.0;
+    double acc = 0.0;
+    for (int cg = wave; cg < ncg; cg += NW) {
+      const int c0 = cg * 8;
+      double g[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int c = c0 + t;
+        g[t] = (c < cmax && r >= c && r < k) ? P[pk_col(c, kc) + (r - c)] : 0.0;
+      }
+      double up[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int c = c0 + t;
+        acc += g[t] * (c < cmax ? x[c] : 0.0);
+        up[t] = (r > c) ? g[t] * xr : 0.0;
+      }
+      double a4[4], a2[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool hi = lane & 32;
+        a4[i] = (hi ? up[i + 4] : up[i]) + __shfl_xor(hi ? up[i] : up[i + 4], 32, 64);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool hi = lane & 16;
+        a2[i] = (hi ? a4[i + 2] : a4[i]) + __shfl_xor(hi ? a4[i] : a4[i + 2], 16, 64);
+      }
+      const bool h3 = lane & 8;
+      double v = (h3 ? a2[1] : a2[0]) + __shfl_xor(h3 ? a2[0] : a2[1], 8, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 1, 64);
+      if ((lane & 7) == 0) {
+        const int c = c0 + ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+        if (c < cmax) upper[wave * ks + c] += v;
+      }
+    }
+    if (r < k) part[wave * ks + r] += acc;
+  }
+  __syncthreads();
+  double d[1] = {0.0};
+  for (int rr = threadIdx.x; rr < k; rr += NW * 64) {
+    double sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += part[w * ks + rr] + upper[w * ks + rr];
+    out[rr] = sum;
+    if (y) d[0] += y[rr] * sum;
+  }
+  block_sums<1, NW>(d, red);
+  return d[0];
+}
+
+// KB > 0 fixes the LDS layout at compile time for modules of at most KB nodes
+// (every carve-out an immediate offset; frees the SGPRs runtime offsets cost).
+template <int NW, bool PACKED, int KB>
+__device__ __forceinline__ void profile_body(const ProfileParams& P) {
+  constexpr int BS = NW * 64;
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int kmax = P.k_max, mmax = P.m_max, S = (int)P.n_samples;
-  double* red = reinterpret_cast<double*>(smem);        // 8 * NR_WAVES
-  double* q = red + 8 * NR_WAVES;                        // [kmax] current Lanczos vector
+  const int kmax = KB > 0 ? KB : P.k_max;
+  const int mmax = KB > 0 ? (KB < 160 ? KB : 160) : P.m_max;
+  const int S = (int)P.n_samples;
+  double* red = reinterpret_cast<double*>(smem);        // 8 * NW
+  double* q = red + 8 * NW;                        // [kmax] current Lanczos vector
   double* qprev = q + kmax;                              // [kmax] previous Lanczos vector
   double* w = qprev + kmax;                              // [kmax]
   double* vv = w + kmax;                                 // [kmax] Ritz vector
   double* gv = vv + kmax;                                // [kmax] G v
   double* colm = gv + kmax;                              // [kmax] column means
-  double* part = colm + kmax;                            // [NR_WAVES * kmax] matvec partials
-  double* alpha = part + NR_WAVES * kmax;                // [mmax]
+  double* part = colm + kmax;                            // [NW * kmax] matvec partials
+  double* upper = part + NW * kmax;                      // [NW * kmax] (packed only)
+  double* alpha = upper + (PACKED ? NW * kmax : 0);      // [mmax]
   double* beta = alpha + mmax;                           // [mmax]
   double* h = beta + mmax;                               // [mmax]
   double* ty = h + mmax;                                 // [mmax]
   double* twork = ty + mmax;                             // [5 * mmax]
-  uint32_t* idx = reinterpret_cast<uint32_t*>(twork + 5 * mmax);  // [kmax]
+  double* omg = twork + 5 * mmax;                        // [3 * (mmax + 1)] omega rows
+  uint32_t* idx = reinterpret_cast<uint32_t*>(omg + 3 * (mmax + 1));  // [kmax]
   __shared__ int s_item;
   __shared__ int s_flag;
   __shared__ int s_done;
+  __shared__ int s_reorth;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;   // Gram (ld x ld)
+  double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;   // Gram
   const int ld = P.ld;
-  double* Q = G + (int64_t)ld * ld;                                 // Lanczos basis
+  double* Q = G + P.gram_doubles;                                   // Lanczos basis
   const double* __restrict__ X = P.data;
   const double Sd = (double)S;
 
@@ -594,7 +748,7 @@ module_profile_kernel(ProfileParams P) {
 
     nr_prp_key key;
     if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
-    for (int c = tid; c < k; c += NR_BS) idx[c] = node_index(P.src, key, p_local, off + c);
+    for (int c = tid; c < k; c += BS) idx[c] = node_index(P.src, key, p_local, off + c);
     if (tid == 0) s_flag = 0;
     __syncthreads();
     NR_STAMP(0);  // queue + index derivation
@@ -602,30 +756,32 @@ module_profile_kernel(ProfileParams P) {
     // ---- Gram [X 1]^T [X 1] on the matrix cores ----
     double g1[1] = {0.0};
     int bad = 0;
-    gram_mfma(X, S, idx, k, G, ld, g1[0], bad);
+    gram_mfma<NW, PACKED>(X, S, idx, k, G, ld, g1[0], bad);
+    const int kc = k + 1;
     if (bad) atomicOr(&s_flag, 1);
-    block_sums<1>(g1, red);      // barriers also publish G to the whole workgroup
+    block_sums<1, NW>(g1, red);      // barriers also publish G to the whole workgroup
     const double ones_g_ones = g1[0];
     NR_STAMP(1);  // Gram
     // svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235)
     const bool nonfinite = s_flag != 0;
 
     if (!nonfinite) {
-      for (int c = tid; c < k; c += NR_BS) colm[c] = G[k + (int64_t)c * ld] / Sd;
+      for (int c = tid; c < k; c += BS)
+        colm[c] = (PACKED ? G[pk_at(k, c, kc)] : G[k + (int64_t)c * ld]) / Sd;
       // ---- Lanczos with full reorthogonalisation (3-term update + one CGS pass) ----
       const int mcap = k < mmax ? k : mmax;
       double nq[1] = {0.0};
-      for (int c = tid; c < k; c += NR_BS) {
+      for (int c = tid; c < k; c += BS) {
         const uint32_t hsh = nr_lowbias32((uint32_t)c * 0x9E3779B9u + 0x1234567u);
         const double v = 1.0 + 0.01 * ((double)(hsh & 0xFFFF) / 65536.0 - 0.5);
         q[c] = v;
         qprev[c] = 0.0;
         nq[0] += v * v;
       }
-      block_sums<1>(nq, red);
+      block_sums<1, NW>(nq, red);
       {
         const double inv = 1.0 / sqrt(nq[0]);
-        for (int c = tid; c < k; c += NR_BS) q[c] *= inv;
+        for (int c = tid; c < k; c += BS) q[c] *= inv;
       }
       if (tid == 0) s_done = 0;
       __syncthreads();
@@ -634,14 +790,43 @@ module_profile_kernel(ProfileParams P) {
       // Convergence of the top Ritz pair is tested at step 16 and every 8 steps
       // after (each test is a tridiagonal eigen-solve on one wave).
       int next_check = mcap < 16 ? mcap : 16;
+      const double sqrt_eps = 1.4901161193847656e-08;
+      bool force_next = false;
+      double anorm = 0.0;
+      if (tid == 0) {
+        omg[0] = 1.0;                                    // omega_{0,0}
+        s_reorth = 0;
+      }
       for (int j = 0; j < mcap; ++j) {
-        for (int c = tid; c < k; c += NR_BS) Q[(int64_t)j * k + c] = q[c];
+        for (int c = tid; c < k; c += BS) Q[(int64_t)j * k + c] = q[c];
         NR_STAMP(2);  // Lanczos: vector updates / tridiagonal checks
-        const double alpha0 = matvec(G, ld, k, q, w, part, kmax, q, red);
+        const double alpha0 = PACKED ? packed_matvec<NW>(G, kc, k, q, w, part, upper, kmax, q, red)
+                                     : matvec(G, ld, k, q, w, part, kmax, q, red);
         NR_STAMP(3);  // Lanczos: matvec
-        const double nb = reorthogonalise(Q, k, j + 1, w, q, qprev, alpha0, beta_prev, h, red);
+        double nb = three_term<NW>(k, w, q, qprev, alpha0, beta_prev, red);
+        double alpha_j = alpha0;
+        double* om_cur = omg + (j % 3) * (mmax + 1);
+        double* om_prev = omg + ((j + 2) % 3) * (mmax + 1);
+        double* om_next = omg + ((j + 1) % 3) * (mmax + 1);
+        anorm = fmax(anorm, fabs(alpha0) + sqrt(nb) + beta_prev);
+        if (tid == 0) alpha[j] = alpha0;
+        __syncthreads();
+        if (wave == 0) {
+          const double mx = omega_update(alpha, beta, j, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
+          if (lane == 0) s_reorth = force_next || mx > sqrt_eps;
+        }
+        __syncthreads();
+        if (s_reorth) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
+          nb = reorthogonalise<NW>(Q, k, j + 1, w, h, red);
+          alpha_j += h[j];
+          if (wave == 0) {
+            const double eps = 2.220446049250313e-16;
+            for (int i = lane; i <= j; i += 64) om_next[i] = eps;
+          }
+          force_next = !force_next;
+          if (P.diag && tid == 0) atomicAdd(P.diag + 3, 1);
+        }
         NR_STAMP(4);  // Lanczos: reorthogonalisation
-        const double alpha_j = alpha0 + h[j];
         const double beta_j = sqrt(nb);
         if (tid == 0) {
           alpha[j] = alpha_j;
@@ -666,7 +851,7 @@ module_profile_kernel(ProfileParams P) {
           if (s_done) break;
         }
         const double inv = 1.0 / beta_j;
-        for (int c = tid; c < k; c += NR_BS) {
+        for (int c = tid; c < k; c += BS) {
           qprev[c] = q[c];
           q[c] = w[c] * inv;
         }
@@ -680,26 +865,27 @@ module_profile_kernel(ProfileParams P) {
       }
       // Ritz vector v = Q y, normalised, then G v
       double nv[1] = {0.0};
-      for (int c = tid; c < k; c += NR_BS) {
+      for (int c = tid; c < k; c += BS) {
         double s = 0.0;
         for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
         vv[c] = s;
         nv[0] += s * s;
       }
-      block_sums<1>(nv, red);
+      block_sums<1, NW>(nv, red);
       {
         const double inv = 1.0 / sqrt(nv[0]);
-        for (int c = tid; c < k; c += NR_BS) vv[c] *= inv;
+        for (int c = tid; c < k; c += BS) vv[c] *= inv;
       }
       __syncthreads();
-      matvec(G, ld, k, vv, gv, part, kmax, nullptr, red);
+      if (PACKED) packed_matvec<NW>(G, kc, k, vv, gv, part, upper, kmax, nullptr, red);
+      else matvec(G, ld, k, vv, gv, part, kmax, nullptr, red);
       // lambda = v.Gv; ubar = mean of u = X v / sigma
       double a3[2] = {0.0, 0.0};
-      for (int c = tid; c < k; c += NR_BS) {
+      for (int c = tid; c < k; c += BS) {
         a3[0] += vv[c] * gv[c];
         a3[1] += colm[c] * vv[c];
       }
-      block_sums<2>(a3, red);
+      block_sums<2, NW>(a3, red);
       const double lambda = a3[0];
       const double sigma = sqrt(lambda);
       const double ubar = a3[1] / sigma;
@@ -708,23 +894,23 @@ module_profile_kernel(ProfileParams P) {
       // of the covariance is that of sum_j cov(x_j, u); var(meanObs) * k^2 * (S-1)
       // = 1'G1 - (sum of all data)^2 / S.
       double a4[2] = {0.0, 0.0};
-      for (int c = tid; c < k; c += NR_BS) {
+      for (int c = tid; c < k; c += BS) {
         a4[0] += gv[c] / sigma - Sd * colm[c] * ubar;
         a4[1] += colm[c];
       }
-      block_sums<2>(a4, red);
+      block_sums<2, NW>(a4, red);
       const double var_mo = ones_g_ones - Sd * a4[1] * a4[1];
       const bool flip = (a4[0] < 0.0) && (var_mo > 0.0) && (var_u > 0.0);
       const double sgn = flip ? -1.0 : 1.0;
       // NC_j = cor(x_j, u) (src/netStats.cpp:279); node order = CSR order
-      for (int c = tid; c < k; c += NR_BS) {
-        const double gjj = G[c + (int64_t)c * ld];
+      for (int c = tid; c < k; c += BS) {
+        const double gjj = PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
         const double cov = gv[c] / sigma - Sd * colm[c] * ubar;
         const double var_x = gjj - Sd * colm[c] * colm[c];
         w[c] = sgn * cov / (sqrt(var_x) * sqrt(var_u));
       }
       if (P.sp_out) {
-        for (int r = tid; r < S; r += NR_BS) {
+        for (int r = tid; r < S; r += BS) {
           double s = 0.0;
           for (int c = 0; c < k; ++c) s += X[(int64_t)idx[c] * S + r] * vv[c];
           P.sp_out[(int64_t)m * S + r] = sgn * s / sigma;
@@ -732,16 +918,16 @@ module_profile_kernel(ProfileParams P) {
       }
       __syncthreads();
     } else {
-      for (int c = tid; c < k; c += NR_BS) w[c] = nr_nan();
+      for (int c = tid; c < k; c += BS) w[c] = nr_nan();
       if (P.sp_out)
-        for (int r = tid; r < S; r += NR_BS) P.sp_out[(int64_t)m * S + r] = nr_nan();
+        for (int r = tid; r < S; r += BS) P.sp_out[(int64_t)m * S + r] = nr_nan();
       __syncthreads();
     }
 
     // ModuleCoherence (src/netStats.cpp:293-305), Correlation / SignAwareMean
     // against the discovery contribution (src/permutations.cpp:99,101).
     double b1[5] = {0, 0, 0, 0, 0};  // nfinite, sum nc^2, ncc, sx, sy
-    for (int c = tid; c < k; c += NR_BS) {
+    for (int c = tid; c < k; c += BS) {
       const double y = w[c];
       if (isfinite(y)) { b1[0] += 1.0; b1[1] += y * y; }
       if (P.disc_nc) {
@@ -750,13 +936,13 @@ module_profile_kernel(ProfileParams P) {
       }
       if (P.nc_out) P.nc_out[off + c] = y;
     }
-    block_sums<5>(b1, red);
+    block_sums<5, NW>(b1, red);
     const double stat_coh = b1[0] >= 1.0 ? b1[1] / b1[0] : nr_nan();
     double stat_cc = nr_nan(), stat_ac = nr_nan();
     if (P.disc_nc && P.out) {
       const double mx = b1[3] / b1[2], my = b1[4] / b1[2];
       double b2[4] = {0, 0, 0, 0};
-      for (int c = tid; c < k; c += NR_BS) {
+      for (int c = tid; c < k; c += BS) {
         const double y = w[c], xv = P.disc_nc[off + c];
         if (isfinite(xv) && isfinite(y)) {
           const double dx = xv - mx, dy = y - my;
@@ -766,7 +952,7 @@ module_profile_kernel(ProfileParams P) {
           b2[3] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
         }
       }
-      block_sums<4>(b2, red);
+      block_sums<4, NW>(b2, red);
       stat_cc = b1[2] >= 1.0 ? b2[2] / (sqrt(b2[0]) * sqrt(b2[1])) : nr_nan();
       stat_ac = b1[2] >= 1.0 ? b2[3] / b1[2] : nr_nan();
     }
@@ -782,6 +968,20 @@ module_profile_kernel(ProfileParams P) {
     __syncthreads();
     NR_STAMP(5);  // Ritz vector, contributions, statistics
   }
+}
+
+__global__ void __launch_bounds__(NR_BS, 3)
+module_profile_kernel(ProfileParams P) {
+  profile_body<NR_WAVES, false, 0>(P);
+}
+
+// Packed-Gram variant: 8-wave workgroups, two per CU, so the live Gram
+// working set stays in the Infinity Cache while Lanczos streams it.
+// OCC = waves per SIMD: 4 -> two workgroups per CU (VGPR-capped at 128), 2 -> one.
+template <int KB, int OCC>
+__global__ void __launch_bounds__(512, OCC)
+module_profile_packed_kernel(ProfileParams P) {
+  profile_body<8, true, KB>(P);
 }
 
 // ---------------------------------------------------------------------------
@@ -874,9 +1074,17 @@ size_t net_kernel_lds(int k_max) {
   return sizeof(double) * (8 * NR_WAVES + (size_t)NR_WAVES * k_max) + sizeof(uint32_t) * k_max;
 }
 
-size_t profile_kernel_lds(int k_max, int m_max, int n_samples) {
+// Compile-time module-size bucket of the packed kernel (0 = runtime layout).
+int packed_bucket(int k_max) { return k_max <= 320 ? 320 : 0; }
+
+size_t profile_kernel_lds(int k_max, int m_max, int n_samples, bool packed) {
   (void)n_samples;
-  return sizeof(double) * (8 * NR_WAVES + (6 + NR_WAVES) * (size_t)k_max + 9 * (size_t)m_max) +
+  const int nw = packed ? 8 : NR_WAVES;
+  if (packed && packed_bucket(k_max) > 0) {
+    k_max = packed_bucket(k_max);
+    m_max = k_max < 160 ? k_max : 160;
+  }
+  return sizeof(double) * (8 * nw + (6 + (packed ? 2 : 1) * nw) * (size_t)k_max + 12 * (size_t)m_max + 3) +
          sizeof(uint32_t) * k_max;
 }
 
@@ -886,9 +1094,21 @@ hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_profile(const ProfileParams& P, int n_slots, hipStream_t st) {
-  const size_t lds = profile_kernel_lds(P.k_max, P.m_max, (int)P.n_samples);
-  hipLaunchKernelGGL(module_profile_kernel, dim3((unsigned)n_slots), dim3(NR_BS), lds, st, P);
+hipError_t launch_profile(const ProfileParams& P, int n_slots, bool packed, int wg_per_cu,
+                          hipStream_t st) {
+  const size_t lds = profile_kernel_lds(P.k_max, P.m_max, (int)P.n_samples, packed);
+  const dim3 g((unsigned)n_slots), b(512);
+  const bool b320 = packed_bucket(P.k_max) == 320;
+  if (packed && b320 && wg_per_cu >= 2)
+    hipLaunchKernelGGL((module_profile_packed_kernel<320, 4>), g, b, lds, st, P);
+  else if (packed && b320)
+    hipLaunchKernelGGL((module_profile_packed_kernel<320, 2>), g, b, lds, st, P);
+  else if (packed && wg_per_cu >= 2)
+    hipLaunchKernelGGL((module_profile_packed_kernel<0, 4>), g, b, lds, st, P);
+  else if (packed)
+    hipLaunchKernelGGL((module_profile_packed_kernel<0, 2>), g, b, lds, st, P);
+  else
+    hipLaunchKernelGGL(module_profile_kernel, dim3((unsigned)n_slots), dim3(NR_BS), lds, st, P);
   return hipGetLastError();
 }
 

@@ -198,9 +198,9 @@ class Engine:
         return ms.value, launches.value, items.value
 
     def diagnostics(self):
-        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
-        self._check(self._lib.nr_get_diagnostics(self._h, C.byref(a), C.byref(b), C.byref(c)))
-        return {"eig_items": a.value, "eig_steps": b.value, "eig_cap_hits": c.value}
+        a, b, c, d = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        self._check(self._lib.nr_get_diagnostics(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return {"eig_items": a.value, "eig_steps": b.value, "eig_cap_hits": c.value, "eig_reorths": d.value}
 
     def set_stamps(self, enable: bool):
         self._check(self._lib.nr_set_stamps(self._h, int(bool(enable))))

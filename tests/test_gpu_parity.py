@@ -245,3 +245,33 @@ def test_constant_column_gives_na():
     _, exp = O.permutation_procedure(disc, tx, tc, tn, mi, np.zeros((0, mi.null_idx.size), int))
     assert_stats_close(obs, exp, what="observed with NaN column")
     assert not np.isfinite(obs[0, [1, 4, 6]]).any()
+
+
+@pytest.mark.parametrize("seed", [11])
+def test_large_modules_vs_cpp_oracle(seed):
+    """C3-like module sizes (k up to 300, S = 200) on a 4,000-node dataset:
+    the Lanczos eigen-solver path at the sizes the benchmark runs, checked
+    against the C++ restatement (LAPACK dgesdd) on identical shuffles."""
+    from netrep_amd import synthetic as S
+    from oracle import ref_cpp
+    sizes = [300, 260, 200, 150, 90, 40, 31]
+    lay = S.make_layout(4000, sizes, seed)
+    dx, dc, dn = S.numpy_dataset(lay, 200, seed + 1)
+    tx, tc, tn = S.numpy_dataset(lay, 200, seed + 2, preserve_all=False)
+    mi = O.ModuleIndex(lay.names, lay.labels, lay.names, lay.modules)
+    disc = O.intermediate_properties(O.scale(dx), dc, dn, mi.disc_idx(lay.names))
+    txs = O.scale(tx)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    seed_p = 2024
+    nulls = eng.run(100, 106, seed_p)
+    pis = N.prp_table(seed_p, 100, 106, mi.null_idx.size)
+    mods = mi.mods_present
+    node_off = np.concatenate([[0], np.cumsum([mi.test_idx[m].size for m in mods])])
+    exp, obs = ref_cpp.permutation_procedure(
+        txs, tc, tn, len(mi.modules), [mi.modules.index(m) for m in mods], node_off,
+        np.concatenate([mi.test_idx[m] for m in mods]), np.concatenate([mi.null_pos[m] for m in mods]),
+        mi.null_idx, np.concatenate([disc["corr"][m] for m in mods]),
+        np.concatenate([disc["degree"][m] for m in mods]),
+        np.concatenate([disc["contribution"][m] for m in mods]), 6, pi=pis, n_threads=8)
+    assert_stats_close(eng.observed(), obs, what="observed (large modules)")
+    assert_stats_close(nulls, exp, what="nulls (large modules)")

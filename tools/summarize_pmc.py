@@ -1,0 +1,65 @@
+"""Summarise tools/collect_pmc.sh output per engine kernel (mean per dispatch).
+
+FETCH_SIZE/WRITE_SIZE are in KB. Following MI355X_MICROARCH.md (HBM section),
+FETCH_SIZE reads 1/2 of the bytes of wide coalesced streams on gfx950; the
+`hbm_bytes_corrected` column doubles it (exact for the wide streaming kernels,
+an upper estimate for narrow random reads, whose ratio is uncalibrated).
+
+  python tools/summarize_pmc.py <out_dir> [--json file]
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(path):
+    agg = defaultdict(lambda: defaultdict(list))
+    if not os.path.exists(path):
+        return agg
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"]
+        if not (name.startswith("nr::") or "nr::" in name[:60]):
+            continue
+        key = name.split("(")[0].replace("void ", "")
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main():
+    out = sys.argv[1]
+    res = defaultdict(dict)
+    for sub in ("fetch", "write", "tcc", "sq", "mfma"):
+        for k, cs in load(os.path.join(out, sub, "run_counter_collection.csv")).items():
+            for c, v in cs.items():
+                res[k][c] = sum(v) / len(v)
+                res[k]["dispatches_" + sub] = len(v)
+    stats = os.path.join(out, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        for r in csv.DictReader(open(stats)):
+            if "nr::" in r["Name"]:
+                key = r["Name"].split("(")[0].replace("void ", "")
+                res[key]["avg_ns"] = float(r["AverageNs"])
+                res[key]["calls"] = int(r["Calls"])
+    for k, d in res.items():
+        if "FETCH_SIZE" in d:
+            d["hbm_bytes_corrected"] = d["FETCH_SIZE"] * 1024 * 2 + d.get("WRITE_SIZE", 0.0) * 1024
+        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
+            d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
+            d["mfma_busy_pct"] = 100 * d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] * 1024)
+        if "SQ_WAVE_CYCLES" in d:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in d:
+                    d[c + "_frac"] = d[c] / max(d["SQ_WAVE_CYCLES"], 1)
+    for k in sorted(res):
+        print(k)
+        for c, v in sorted(res[k].items()):
+            print(f"   {c:36s} {v:.6g}")
+    if "--json" in sys.argv:
+        json.dump(res, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
