@@ -37,6 +37,12 @@ struct DeviceTimer {
 struct nr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // The gather (network) kernel runs on `side`, concurrently with the
+  // summary-profile kernel on `stream`: one is bound by random 64 B HBM
+  // reads, the other by streaming its per-slot Gram, so they overlap.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool concurrent = true;
   std::string err;
   std::mutex mu;
 
@@ -83,6 +89,7 @@ struct nr_ctx {
   bool timing = false;
   unsigned long long* d_stamps = nullptr;  // phase stamps (nr_set_stamps)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ev_pending[2] = {false, false};
   DeviceTimer timers[2];
 };
 
@@ -159,12 +166,14 @@ int profile_m_max(int k_max) { return std::min(k_max, 160); }
 // padded to a 32-column super-tile.
 int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
 
-// Launch plan of the summary-profile kernel. Default: the full-Gram variant
-// (4-wave workgroups, 3 per CU), measured fastest at C3. The packed variant
-// (8-wave workgroups, packed symmetric Gram, half the Lanczos bytes) is kept
-// for A/B measurement: NETREP_PROFILE_VARIANT=packed (NETREP_PACKED_WG_PER_CU).
+// Launch plan of the summary-profile kernel. Default: packed symmetric Gram
+// (half the Lanczos bytes) in 4-wave workgroups, 3 per CU -- measured fastest
+// at C3 (30.5 ms vs 34.2 ms full-Gram per 256 permutations). The full-Gram
+// 4-wave and packed 8-wave variants stay for A/B measurement and as the
+// fallback when the packed layout does not fit LDS:
+// NETREP_PROFILE_VARIANT=full|packed|packed4, NETREP_PROFILE_WG_PER_CU.
 struct ProfilePlan {
-  bool packed = false;
+  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave
   int slots = 0;
   int per_cu = 1;
   int64_t gram_doubles = 0, stride = 0;
@@ -174,23 +183,24 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
   const int m = profile_m_max(k_max);
-  const size_t lds_packed = nr::profile_kernel_lds(k_max, m, n_samples, true);
-  const size_t lds_full = nr::profile_kernel_lds(k_max, m, n_samples, false);
-  const char* force = std::getenv("NETREP_PROFILE_VARIANT");
-  bool packed = false;
-  if (force && std::string(force) == "full") packed = false;
-  if (force && std::string(force) == "packed" && lds_packed <= 160 * 1024) packed = true;
-  const size_t lds = packed ? lds_packed : lds_full;
+  int variant = 2;
+  if (const char* f = std::getenv("NETREP_PROFILE_VARIANT")) {
+    const std::string v(f);
+    variant = v == "packed" ? 1 : v == "full" ? 0 : 2;
+  }
+  if (variant != 0 && nr::profile_kernel_lds(k_max, m, n_samples, variant) > 160 * 1024) variant = 0;
+  const size_t lds = nr::profile_kernel_lds(k_max, m, n_samples, variant);
   if (lds > 160 * 1024)
     return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
-  int want = packed ? 2 : 3;
-  if (const char* e = std::getenv("NETREP_PACKED_WG_PER_CU"))
-    if (packed) want = std::max(1, std::min(2, std::atoi(e)));
+  int want = variant == 1 ? 2 : 3;
+  if (const char* e = std::getenv("NETREP_PROFILE_WG_PER_CU")) want = std::max(1, std::min(3, std::atoi(e)));
+  if (variant == 1) want = std::min(want, 2);
+  if (variant == 2) want = std::max(2, want);
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
-  plan->packed = packed;
+  plan->variant = variant;
   plan->per_cu = per_cu;
   plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu));
-  if (packed) {
+  if (variant != 0) {
     const int64_t kc = k_max + 1;
     plan->gram_doubles = (kc * (kc + 1) / 2 + 31) / 32 * 32;
   } else {
@@ -201,19 +211,30 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
 }
 
-void timer_begin(nr_ctx* ctx, int which) {
-  if (ctx->timing) (void)hipEventRecord(ctx->ev[2 * which], ctx->stream);
+// Kernel timers: events on the kernel's own stream; collected (synchronised)
+// only after both kernels of a batch are enqueued, so timing does not
+// serialise the two streams.
+void timer_begin(nr_ctx* ctx, int which, hipStream_t st) {
+  if (ctx->timing) (void)hipEventRecord(ctx->ev[2 * which], st);
 }
 
-void timer_end(nr_ctx* ctx, int which, int64_t items) {
+void timer_end(nr_ctx* ctx, int which, int64_t items, hipStream_t st) {
   if (!ctx->timing) return;
-  (void)hipEventRecord(ctx->ev[2 * which + 1], ctx->stream);
-  (void)hipEventSynchronize(ctx->ev[2 * which + 1]);
-  float ms = 0.f;
-  (void)hipEventElapsedTime(&ms, ctx->ev[2 * which], ctx->ev[2 * which + 1]);
-  ctx->timers[which].ms += ms;
+  (void)hipEventRecord(ctx->ev[2 * which + 1], st);
+  ctx->ev_pending[which] = true;
   ctx->timers[which].launches += 1;
   ctx->timers[which].items += items;
+}
+
+void timer_collect(nr_ctx* ctx) {
+  for (int which = 0; which < 2; ++which) {
+    if (!ctx->ev_pending[which]) continue;
+    ctx->ev_pending[which] = false;
+    (void)hipEventSynchronize(ctx->ev[2 * which + 1]);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ctx->ev[2 * which], ctx->ev[2 * which + 1]);
+    ctx->timers[which].ms += ms;
+  }
 }
 
 nr::IndexSource make_source(const nr_ctx* ctx, int mode, uint64_t seed, int64_t perm_base,
@@ -263,9 +284,15 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   np.slot_cor_degree = data ? 3 : 2;
   np.slot_avg_cor = data ? 5 : 3;
   np.out = d_out;
-  timer_begin(ctx, 0);
-  NR_HIP(ctx, nr::launch_net(np, n_items, ctx->stream));
-  timer_end(ctx, 0, n_items);
+  const bool fork = data && ctx->concurrent;
+  hipStream_t net_stream = fork ? ctx->side : ctx->stream;
+  if (fork) {
+    NR_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+    NR_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  }
+  timer_begin(ctx, 0, net_stream);
+  NR_HIP(ctx, nr::launch_net(np, n_items, net_stream));
+  timer_end(ctx, 0, n_items, net_stream);
 
   if (data) {
     ProfilePlan plan;
@@ -297,10 +324,15 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.queue = ctx->d_counters;
     pp.diag = ctx->d_counters + 1;
     pp.stamps = ctx->d_stamps;
-    timer_begin(ctx, 1);
-    NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.packed, plan.per_cu, ctx->stream));
-    timer_end(ctx, 1, n_items);
+    timer_begin(ctx, 1, ctx->stream);
+    NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, ctx->stream));
+    timer_end(ctx, 1, n_items, ctx->stream);
   }
+  if (fork) {
+    NR_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
+    NR_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  }
+  timer_collect(ctx);
   return NR_OK;
 }
 
@@ -404,6 +436,10 @@ int nr_ctx_create(int device, nr_ctx** out) {
   ctx->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
+  if (const char* c = std::getenv("NETREP_CONCURRENT")) ctx->concurrent = std::atoi(c) != 0;
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, 16 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, 16 * sizeof(int));
@@ -420,6 +456,7 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   dfree(ctx->d_pairs);
   dfree(ctx->d_data);
   dfree(ctx->d_row_of);
@@ -441,6 +478,9 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   for (auto& ev : ctx->ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -724,7 +764,7 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
       pp.scratch_stride = plan.stride;
       pp.queue = ctx->d_counters;
       pp.diag = ctx->d_counters + 1;
-      if (e == hipSuccess) e = nr::launch_profile(pp, plan.slots, plan.packed, plan.per_cu, ctx->stream);
+      if (e == hipSuccess) e = nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, ctx->stream);
     }
     auto d2h = [&](double* h, const double* d, int64_t n) {
       if (e == hipSuccess && h && n > 0)

@@ -68,9 +68,9 @@ struct ProfileParams {
 };
 
 size_t net_kernel_lds(int k_max);
-size_t profile_kernel_lds(int k_max, int m_max, int n_samples, bool packed);
+size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant);
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
-hipError_t launch_profile(const ProfileParams& P, int n_slots, bool packed, int wg_per_cu,
+hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);
 hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,
                              hipStream_t st);

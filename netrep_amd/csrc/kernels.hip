@@ -984,6 +984,13 @@ module_profile_packed_kernel(ProfileParams P) {
   profile_body<8, true, KB>(P);
 }
 
+// Packed Gram in the lean 4-wave structure (OCC workgroups per CU).
+template <int KB, int OCC>
+__global__ void __launch_bounds__(NR_BS, OCC)
+module_profile_packed4_kernel(ProfileParams P) {
+  profile_body<NR_WAVES, true, KB>(P);
+}
+
 // ---------------------------------------------------------------------------
 // Support kernels
 // ---------------------------------------------------------------------------
@@ -1077,9 +1084,11 @@ size_t net_kernel_lds(int k_max) {
 // Compile-time module-size bucket of the packed kernel (0 = runtime layout).
 int packed_bucket(int k_max) { return k_max <= 320 ? 320 : 0; }
 
-size_t profile_kernel_lds(int k_max, int m_max, int n_samples, bool packed) {
+// variant: 0 full Gram (4 waves), 1 packed (8 waves), 2 packed (4 waves)
+size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
   (void)n_samples;
-  const int nw = packed ? 8 : NR_WAVES;
+  const bool packed = variant != 0;
+  const int nw = variant == 1 ? 8 : NR_WAVES;
   if (packed && packed_bucket(k_max) > 0) {
     k_max = packed_bucket(k_max);
     m_max = k_max < 160 ? k_max : 160;
@@ -1094,11 +1103,21 @@ hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_profile(const ProfileParams& P, int n_slots, bool packed, int wg_per_cu,
+hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st) {
-  const size_t lds = profile_kernel_lds(P.k_max, P.m_max, (int)P.n_samples, packed);
-  const dim3 g((unsigned)n_slots), b(512);
+  const size_t lds = profile_kernel_lds(P.k_max, P.m_max, (int)P.n_samples, variant);
+  const dim3 g((unsigned)n_slots), b(512), b4(NR_BS);
   const bool b320 = packed_bucket(P.k_max) == 320;
+  const bool packed = variant == 1;
+  if (variant == 2) {
+    if (b320 && wg_per_cu >= 3)
+      hipLaunchKernelGGL((module_profile_packed4_kernel<320, 3>), g, b4, lds, st, P);
+    else if (b320)
+      hipLaunchKernelGGL((module_profile_packed4_kernel<320, 2>), g, b4, lds, st, P);
+    else
+      hipLaunchKernelGGL((module_profile_packed4_kernel<0, 2>), g, b4, lds, st, P);
+    return hipGetLastError();
+  }
   if (packed && b320 && wg_per_cu >= 2)
     hipLaunchKernelGGL((module_profile_packed_kernel<320, 4>), g, b, lds, st, P);
   else if (packed && b320)
