@@ -37,12 +37,13 @@ struct DeviceTimer {
 struct nr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  // The gather (network) kernel runs on `side`, concurrently with the
-  // summary-profile kernel on `stream`: one is bound by random 64 B HBM
-  // reads, the other by streaming its per-slot Gram, so they overlap.
+  // NETREP_CONCURRENT=1 runs the gather (network) kernel on `side`,
+  // concurrently with the summary-profile kernel. Off by default: measured
+  // at C3 it costs 14% (6,090 vs 7,077 perms/s) because the gather kernel's
+  // workgroups take CU slots from the persistent profile grid.
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool concurrent = true;
+  bool concurrent = false;
   std::string err;
   std::mutex mu;
 

@@ -279,10 +279,13 @@ def net_props(data, net, node_names, module_nodes, modules):
         names = module_nodes[m]
         pres = [i for i, n in enumerate(names) if n in n_idx]     # propIdx :104
         node_idx = np.array([n_idx[names[i]] for i in pres], dtype=np.int64)
-        degree = np.full(len(names), np.nan)
-        contribution = np.full(len(names), np.nan)
-        summary = np.full(n_samples, np.nan)
-        avg_weight = coherence = np.nan
+        # NA-initialised results (:86-90); computed degree/avgWeight are kept
+        # as computed (no NaN->NA step for them, :121-138), so e.g. a
+        # one-node module has avgWeight 0/0 = NaN, not NA.
+        degree = np.full(len(names), NA_REAL)
+        contribution = np.full(len(names), NA_REAL)
+        summary = np.full(n_samples, NA_REAL)
+        avg_weight = coherence = NA_REAL
         if node_idx.size > 0:
             srt, rank = sort_nodes(node_idx)
             wd = weighted_degree(net, srt)[rank]
@@ -294,7 +297,7 @@ def net_props(data, net, node_names, module_nodes, modules):
                 coherence = module_coherence(nc)
                 contribution[pres] = nc
                 summary = sp
-        entry = {"degree": na_fill(degree), "avgWeight": na_fill([avg_weight])[0]}
+        entry = {"degree": degree, "avgWeight": avg_weight}
         if data is not None:
             entry.update(summary=na_fill(summary), contribution=na_fill(contribution),
                          coherence=na_fill([coherence])[0])

@@ -275,3 +275,28 @@ def test_large_modules_vs_cpp_oracle(seed):
         np.concatenate([disc["contribution"][m] for m in mods]), 6, pi=pis, n_threads=8)
     assert_stats_close(eng.observed(), obs, what="observed (large modules)")
     assert_stats_close(nulls, exp, what="nulls (large modules)")
+
+
+def test_netprops_one_node_and_absent_modules(bundled):
+    """NetProps keeps AverageEdgeWeight's 0/0 = NaN for a one-node module
+    (src/properties.cpp:121, no NaN->NA step for it) and leaves modules with no
+    nodes present NA throughout (:86-90)."""
+    d, ma, t_names = bundled_inputs(bundled)
+    ma = dict(ma)
+    first = t_names[0]
+    ma[first] = "solo"                       # a one-node module
+    ma["not_in_data_1"] = "ghost"            # a module with no node present
+    ma["not_in_data_2"] = "ghost"
+    mods = ["1", "solo", "ghost"]
+    got = N.NetProps(d["tData"], d["tNet"], ma, mods)
+    module_nodes = {m: [n for n, l in ma.items() if l == m] for m in mods}
+    exp = O.net_props(d["tData"].values, d["tNet"].values, t_names, module_nodes, mods)
+    for m in mods:
+        for key in ("summary", "contribution", "degree"):
+            assert_stats_close(got[m][key], exp[m][key], what=f"{m}/{key}")
+        assert_stats_close([got[m]["coherence"]], [exp[m]["coherence"]], what=f"{m}/coherence")
+        assert_stats_close([got[m]["avgWeight"]], [exp[m]["avgWeight"]], what=f"{m}/avgWeight")
+    assert np.isnan(got["solo"]["avgWeight"])
+    na = np.uint64(0x7FF00000000007A2)
+    assert np.float64(got["solo"]["avgWeight"]).view(np.uint64) != na
+    assert np.float64(got["ghost"]["avgWeight"]).view(np.uint64) == na
