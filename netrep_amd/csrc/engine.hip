@@ -203,7 +203,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu));
   if (variant != 0) {
     const int64_t kc = k_max + 1;
-    plan->gram_doubles = (kc * (kc + 1) / 2 + 31) / 32 * 32;
+    plan->gram_doubles = (kc * (kc + 1) / 2 + 1 + 31) / 32 * 32;  // packed triangle + zero pad
   } else {
     const int64_t ld = gram_ld(k_max);
     plan->gram_doubles = ld * ld;

@@ -585,6 +585,7 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
           for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
       }
     }
+    if (PACKED && t == 0 && lane == 0) G[pk_col(kc, kc)] = 0.0;  // zero pad read by packed_matvec
     const double wgt = (I2 == J2) ? 1.0 : 2.0;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -620,63 +621,106 @@ __device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memti
     }                                                                           \
   } while (0)
 
+// Cross-lane butterfly steps without LDS (gfx950): v_permlane32_swap /
+// v_permlane16_swap exchange half-waves / odd-even rows of two registers, so
+// x' + y' leaves lanes [0,32) with x summed over the lane pair (l, l^32) and
+// lanes [32,64) with y summed likewise (16-lane rows for the 16 variant).
+__device__ __forceinline__ double nr_swap32_sum(double x, double y) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(y), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(y), false, false);
+  return __hiloint2double((int)hi[0], (int)lo[0]) + __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ double nr_swap16_sum(double x, double y) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(y), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(y), false, false);
+  return __hiloint2double((int)hi[0], (int)lo[0]) + __hiloint2double((int)hi[1], (int)lo[1]);
+}
+// DPP lane moves within 16-lane rows (both dwords of a double).
+template <int CTRL>
+__device__ __forceinline__ double nr_dpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+constexpr int NR_DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int NR_DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int NR_DPP_ROR8 = 0x128;        // row_ror:8 == lane ^ 8 within a row
+constexpr int NR_DPP_HALF_MIRROR = 0x141; // lane ^ 7 within 8 lanes (flips bit 2)
+
+// Transpose-reduce of 16 per-lane column partials up[0..16) over the 64 rows
+// (lanes) of a unit: afterwards lanes with (lane & 3) == 0 hold the column
+// sum of column 8*b5 + 4*b4 + 2*b3 + b2 (b = lane bits). 8 + 4 swaps, 3 + 2
+// DPP-exchange levels; no LDS traffic.
+__device__ __forceinline__ double nr_transpose_reduce16(const double (&up)[16], int lane) {
+  double a8[8], a4[4], a2[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a8[i] = nr_swap32_sum(up[i], up[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a4[i] = nr_swap16_sum(a8[i], a8[i + 4]);
+  const bool b3 = lane & 8;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    a2[i] = (b3 ? a4[i + 2] : a4[i]) + nr_dpp<NR_DPP_ROR8>(b3 ? a4[i] : a4[i + 2]);
+  const bool b2 = lane & 4;
+  double v = (b2 ? a2[1] : a2[0]) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? a2[0] : a2[1]);
+  v += nr_dpp<NR_DPP_XOR2>(v);
+  v += nr_dpp<NR_DPP_XOR1>(v);
+  return v;
+}
+
 // w = G x over the leading k x k block of the PACKED symmetric G (pk_at), NW
-// waves. Work units are (64-row block, 8-column group) pairs with columns
+// waves. Work units are (64-row block, 16-column group) pairs with columns
 // c <= last row of the block; lanes own rows. One coalesced read of each
 // column segment feeds the lower part (w_r += G_rc x_c, lane-local) and the
-// mirrored upper part (w_c += sum_{r>c} G_rc x_r), the latter reduced for 8
-// columns at once by a transpose-reduce butterfly (10 shuffles). Per-wave
+// mirrored upper part (w_c += sum_{r>c} G_rc x_r), the latter reduced for 16
+// columns at once by the register butterfly above. A unit's 16 loads are
+// issued back to back (no exec-masked lanes: out-of-range lanes read the
+// zero pad element after the triangle), so each wave keeps 16 column
+// segments in flight. Column offsets are wave-uniform (scalar). Per-wave
 // partial arrays keep the sums deterministic. Returns sum_r y_r out_r if y.
 template <int NW>
 __device__ __forceinline__ double packed_matvec(const double* __restrict__ P, int kc, int k,
                                                 const double* x, double* out, double* part,
                                                 double* upper, int ks, const double* y, double* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int i = threadIdx.x; i < NW * ks; i += NW * 64) {
     part[i] = 0.0;
     upper[i] = 0.0;
   }
   __syncthreads();
+  // Raw buffer loads: the column offset is a scalar soffset, the row a 32-bit
+  // voffset; out-of-range lanes get voffset 2^31 and the range check returns 0.
+  const int nrec = (kc * (kc + 1) / 2 + 1) * 8;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P, (short)0, nrec, 0x00020000);
   const int nrb = (k + 63) / 64;
-  for (int rbi = 0; rbi < nrb; ++rbi) {
-    const int r = rbi * 64 + lane;
-    const int cmax = min(k, (rbi + 1) * 64);
-    const int ncg = (cmax + 7) / 8;
-    const double xr = r < k ? x[r] : 0.0;
+  for (int rb = 0; rb < nrb; ++rb) {
+    const int r = rb * 64 + lane;
+    const int cmax = min(k, (rb + 1) * 64);
+    const int ncg = (cmax + 15) / 16;
+    const double xr = x[min(r, k - 1)];  // rows >= k carry g = 0
     double acc = 0.0;
     for (int cg = wave; cg < ncg; cg += NW) {
-      const int c0 = cg * 8;
-      double g[8];
+      const int c0 = cg * 16;
+      double g[16];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
+      for (int t = 0; t < 16; ++t) {
         const int c = c0 + t;
-        g[t] = (c < cmax && r >= c && r < k) ? P[pk_col(c, kc) + (r - c)] : 0.0;
+        const int colbase = c * kc - c * (c - 1) / 2 - c;  // pk_col(c, kc) - c, scalar
+        const bool ok = c < cmax && r >= c && r < k;
+        g[t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                              rsrc, ok ? r * 8 : (int)0x80000000, colbase * 8, 0));
       }
-      double up[8];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
+      for (int t = 0; t < 16; ++t) {
         const int c = c0 + t;
-        acc += g[t] * (c < cmax ? x[c] : 0.0);
-        up[t] = (r > c) ? g[t] * xr : 0.0;
+        acc += g[t] * x[min(c, k - 1)];  // columns >= cmax carry g = 0
+        g[t] = (r > c) ? g[t] * xr : 0.0;  // in place: upper-part partials
       }
-      double a4[4], a2[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool hi = lane & 32;
-        a4[i] = (hi ? up[i + 4] : up[i]) + __shfl_xor(hi ? up[i] : up[i + 4], 32, 64);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const bool hi = lane & 16;
-        a2[i] = (hi ? a4[i + 2] : a4[i]) + __shfl_xor(hi ? a4[i] : a4[i + 2], 16, 64);
-      }
-      const bool h3 = lane & 8;
-      double v = (h3 ? a2[1] : a2[0]) + __shfl_xor(h3 ? a2[0] : a2[1], 8, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 1, 64);
-      if ((lane & 7) == 0) {
-        const int c = c0 + ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+      const double v = nr_transpose_reduce16(g, lane);
+      if ((lane & 3) == 0) {
+        const int c = c0 + ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 +
+                      ((lane >> 2) & 1);
         if (c < cmax) upper[wave * ks + c] += v;
       }
     }
