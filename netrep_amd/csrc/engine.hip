@@ -167,14 +167,16 @@ int profile_m_max(int k_max) { return std::min(k_max, 160); }
 // padded to a 32-column super-tile.
 int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
 
-// Launch plan of the summary-profile kernel. Default: packed symmetric Gram
-// (half the Lanczos bytes) in 4-wave workgroups, 3 per CU -- measured fastest
-// at C3 (30.5 ms vs 34.2 ms full-Gram per 256 permutations). The full-Gram
-// 4-wave and packed 8-wave variants stay for A/B measurement and as the
-// fallback when the packed layout does not fit LDS:
-// NETREP_PROFILE_VARIANT=full|packed|packed4, NETREP_PROFILE_WG_PER_CU.
+// Launch plan of the summary-profile kernel. Default: the packed symmetric
+// Gram in global scratch, 4-wave workgroups, 3 per CU (variant 2; measured
+// fastest at C3: 23.4 ms per 256 permutations). Alternatives for A/B:
+// the register-resident Gram (variant 3, one 8-wave workgroup per CU, the
+// Gram never leaves the registers/LDS of the CU that computed it; modules of
+// <= 303 nodes; 30.5 ms), packed 8-wave (1) and full Gram (0, also the
+// fallback when the packed layout does not fit LDS):
+// NETREP_PROFILE_VARIANT=reg|packed4|packed|full, NETREP_PROFILE_WG_PER_CU.
 struct ProfilePlan {
-  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave
+  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave, 3 register-resident
   int slots = 0;
   int per_cu = 1;
   int64_t gram_doubles = 0, stride = 0;
@@ -187,8 +189,9 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   int variant = 2;
   if (const char* f = std::getenv("NETREP_PROFILE_VARIANT")) {
     const std::string v(f);
-    variant = v == "packed" ? 1 : v == "full" ? 0 : 2;
+    variant = v == "packed" ? 1 : v == "full" ? 0 : v == "reg" ? 3 : 2;
   }
+  if (variant == 3 && k_max > nr::reg_kernel_k_max()) variant = 2;
   if (variant != 0 && nr::profile_kernel_lds(k_max, m, n_samples, variant) > 160 * 1024) variant = 0;
   const size_t lds = nr::profile_kernel_lds(k_max, m, n_samples, variant);
   if (lds > 160 * 1024)
@@ -197,11 +200,14 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   if (const char* e = std::getenv("NETREP_PROFILE_WG_PER_CU")) want = std::max(1, std::min(3, std::atoi(e)));
   if (variant == 1) want = std::min(want, 2);
   if (variant == 2) want = std::max(2, want);
+  if (variant == 3) want = 1;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
   plan->variant = variant;
   plan->per_cu = per_cu;
   plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu));
-  if (variant != 0) {
+  if (variant == 3) {
+    plan->gram_doubles = 0;  // the Gram lives in registers and LDS
+  } else if (variant != 0) {
     const int64_t kc = k_max + 1;
     plan->gram_doubles = (kc * (kc + 1) / 2 + 1 + 31) / 32 * 32;  // packed triangle + zero pad
   } else {

@@ -69,6 +69,7 @@ struct ProfileParams {
 
 size_t net_kernel_lds(int k_max);
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant);
+int reg_kernel_k_max();  // largest module of the register-resident scheme
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);

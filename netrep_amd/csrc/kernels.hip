@@ -247,28 +247,44 @@ __device__ __forceinline__ double nr_rcp(double d) {
 }
 
 // Largest eigenvalue of the symmetric tridiagonal (alpha[0..n), beta[0..n-1))
-// by 64-way multisection on Sturm counts; executed by one full wave.
+// by 64-way multisection on Sturm counts; executed by one full wave. The
+// counts use the characteristic-polynomial recurrence of the Gershgorin-
+// normalised matrix, p_i = (a_i - x) p_{i-1} - b_{i-1}^2 p_{i-2} (sign changes
+// of p_0..p_n = eigenvalues below x): one FMA on the dependency chain per
+// step and no division; |p| is renormalised every 4 steps.
 __device__ double tri_top_eigenvalue(const double* alpha, const double* beta, int n, int lane) {
   double lo = alpha[0], hi = alpha[0];
-  for (int i = 0; i < n; ++i) {
+  for (int i = lane; i < n; i += 64) {
     const double r = (i > 0 ? fabs(beta[i - 1]) : 0.0) + (i < n - 1 ? fabs(beta[i]) : 0.0);
     lo = fmin(lo, alpha[i] - r);
     hi = fmax(hi, alpha[i] + r);
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
   const double scale = fmax(fabs(lo), fabs(hi)) + 1e-300;
+  const double inv = 1.0 / scale;
   lo -= 1e-14 * scale;
   hi += 1e-14 * scale;
-  const double tiny = 1e-300;
   for (int it = 0; it < 12; ++it) {
-    const double x = lo + (hi - lo) * (double)(lane + 1) / 65.0;
-    int cnt = 0;  // eigenvalues < x
-    double d = alpha[0] - x;
-    if (fabs(d) < tiny) d = -tiny;
-    cnt += d < 0.0;
+    const double x = (lo + (hi - lo) * (double)(lane + 1) / 65.0) * inv;
+    double p0 = 1.0, p1 = alpha[0] * inv - x;
+    int cnt = p1 < 0.0;  // eigenvalues < x
+#pragma unroll 4
     for (int i = 1; i < n; ++i) {
-      d = alpha[i] - x - beta[i - 1] * beta[i - 1] * nr_rcp(d);
-      if (fabs(d) < tiny) d = -tiny;
-      cnt += d < 0.0;
+      const double b = beta[i - 1] * inv;
+      const double p2 = fma(alpha[i] * inv - x, p1, -(b * b) * p0);
+      cnt += (p2 < 0.0) != (p1 < 0.0);
+      p0 = p1;
+      p1 = p2;
+      if ((i & 3) == 0) {
+        const double mg = fabs(p1);
+        const double s = mg > 1e150 ? 1e-150 : (mg < 1e-150 ? 1e150 : 1.0);
+        p0 *= s;
+        p1 *= s;
+      }
     }
     // largest x with cnt <= n-1 becomes lo; smallest x with cnt == n becomes hi
     const unsigned long long below = __ballot(cnt <= n - 1);
@@ -281,6 +297,33 @@ __device__ double tri_top_eigenvalue(const double* alpha, const double* beta, in
     if (hi - lo <= 2e-16 * scale) break;
   }
   return 0.5 * (lo + hi);
+}
+
+// Convergence estimate of the top Ritz pair: |last component| of the unit
+// eigenvector y of the tridiagonal for theta, times beta_j. y comes from the
+// three-term recurrence run BACKWARDS from y_{n-1} = 1: the top eigenvector
+// of an unreduced Jacobi matrix is positive and its tail decays once the
+// pair converges, so upward it is the dominant (stable) solution. rb holds
+// 1/beta[0..n-1), one wave fills it. Returns beta_j / |y| (lane 0).
+__device__ double tri_top_resid(const double* alpha, const double* beta, int n, double theta, double beta_j,
+                                double* rb, int lane) {
+  for (int i = lane; i < n - 1; i += 64) rb[i] = 1.0 / beta[i];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double y1 = 1.0, y2 = 0.0, ss = 1.0;  // y_i, y_{i+1}, sum of squares
+  for (int i = n - 1; i > 0; --i) {
+    const double y0 = fma(theta - alpha[i], y1, -(i < n - 1 ? beta[i] : 0.0) * y2) * rb[i - 1];
+    ss = fma(y0, y0, ss);
+    y2 = y1;
+    y1 = y0;
+    if (ss > 1e200) {
+      y1 *= 1e-100;
+      y2 *= 1e-100;
+      ss *= 1e-200;
+      beta_j *= 1e-100;
+    }
+  }
+  return beta_j / sqrt(ss);
 }
 
 // Eigenvector of the tridiagonal for eigenvalue theta by two steps of inverse
@@ -618,19 +661,6 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
   }
 }
 
-// Phase stamps (diagnostics only: active when P.stamps != NULL, a separate
-// measurement run; no stamp executes otherwise). Thread 0 accumulates shader
-// cycles per phase between the barriers that already delimit the phases.
-__device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memtime(); }
-#define NR_STAMP(slot)                                                          \
-  do {                                                                          \
-    if (P.stamps && threadIdx.x == 0) {                                         \
-      const uint64_t t_ = nr_clock();                                           \
-      atomicAdd((unsigned long long*)&P.stamps[slot], (unsigned long long)(t_ - t_mark)); \
-      t_mark = t_;                                                              \
-    }                                                                           \
-  } while (0)
-
 // Cross-lane butterfly steps without LDS (gfx950): v_permlane32_swap /
 // v_permlane16_swap exchange half-waves / odd-even rows of two registers, so
 // x' + y' leaves lanes [0,32) with x summed over the lane pair (l, l^32) and
@@ -818,295 +848,403 @@ __device__ __forceinline__ double reorthogonalise_bf(const double* __restrict__ 
   return nrm[0];
 }
 
+// ---------------------------------------------------------------------------
+// Summary-profile item pipeline, shared by every Gram storage scheme:
+//   index set -> Gram (scheme) -> Lanczos top eigenpair (lanczos_ritz) ->
+//   node contributions (profile_contrib) -> statistics (profile_stats).
+// ---------------------------------------------------------------------------
+
+// LDS carve-out common to all summary-profile bodies.
+struct LzLds {
+  double *red, *q, *qprev, *w, *vv, *gv, *colm;
+  double *alpha, *beta, *h, *ty, *twork, *omg;
+  uint32_t* idx;
+  int mmax;
+};
+
+// Carves red, q, qprev, w, vv, gv, colm (kvec each), then `extra` doubles for
+// the storage scheme (returned in *extra_out), then the Lanczos tridiagonal
+// arrays and idx. Layout matches profile_kernel_lds / reg_kernel_lds.
+template <int NW>
+__device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mmax, int64_t extra,
+                                           double** extra_out) {
+  LzLds L;
+  L.red = reinterpret_cast<double*>(smem);  // 8 * NW
+  L.q = L.red + 8 * NW;
+  L.qprev = L.q + kvec;
+  L.w = L.qprev + kvec;
+  L.vv = L.w + kvec;
+  L.gv = L.vv + kvec;
+  L.colm = L.gv + kvec;
+  *extra_out = L.colm + kvec;
+  L.alpha = *extra_out + extra;  // [mmax]
+  L.beta = L.alpha + mmax;       // [mmax]
+  L.h = L.beta + mmax;           // [mmax]
+  L.ty = L.h + mmax;             // [mmax]
+  L.twork = L.ty + mmax;         // [5 * mmax]
+  L.omg = L.twork + 5 * mmax;    // [3 * (mmax + 1)] omega rows
+  L.idx = reinterpret_cast<uint32_t*>(L.omg + 3 * (mmax + 1));  // [kvec]
+  L.mmax = mmax;
+  return L;
+}
+
+// Phase stamps (diagnostics only: active when P.stamps != NULL, a separate
+// measurement run; no stamp executes otherwise). Thread 0 accumulates shader
+// cycles per phase between the barriers that already delimit the phases.
+__device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memtime(); }
+#define NR_STAMP(slot)                                                          \
+  do {                                                                          \
+    if (P.stamps && threadIdx.x == 0) {                                         \
+      const uint64_t t_ = nr_clock();                                           \
+      atomicAdd((unsigned long long*)&P.stamps[slot], (unsigned long long)(t_ - t_mark)); \
+      t_mark = t_;                                                              \
+    }                                                                           \
+  } while (0)
+
+// Lanczos for the top eigenpair of the k x k operator mv (mv(x, out, y)
+// writes out = G x for rows < k and returns y . out; x is zero beyond k):
+// three-term update, partial reorthogonalisation by the omega recurrence
+// (one CGS pass against the basis Q, k x mcap in global scratch), top Ritz
+// pair of the tridiagonal by Sturm multisection + inverse iteration at
+// predicted convergence checks. Leaves the normalised Ritz vector in L.vv.
+template <int NW, bool BF, class MV>
+__device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, const LzLds& L, int* flags,
+                                             double* Q, MV& mv, uint64_t& t_mark) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mmax = L.mmax;
+  double* q = L.q;
+  double* qprev = L.qprev;
+  double* w = L.w;
+  double* red = L.red;
+  double* alpha = L.alpha;
+  double* beta = L.beta;
+  double* h = L.h;
+  double* ty = L.ty;
+  double* twork = L.twork;
+  double* omg = L.omg;
+  int& s_done = flags[2];
+  int& s_reorth = flags[3];
+  int& s_next_check = flags[4];
+
+  const int mcap = k < mmax ? k : mmax;
+  double nq[1] = {0.0};
+  for (int c = tid; c < k; c += BS) {
+    const uint32_t hsh = nr_lowbias32((uint32_t)c * 0x9E3779B9u + 0x1234567u);
+    const double v = 1.0 + 0.01 * ((double)(hsh & 0xFFFF) / 65536.0 - 0.5);
+    q[c] = v;
+    qprev[c] = 0.0;
+    nq[0] += v * v;
+  }
+  block_sums<1, NW>(nq, red);
+  {
+    const double inv = 1.0 / sqrt(nq[0]);
+    for (int c = tid; c < k; c += BS) q[c] *= inv;
+  }
+  if (tid == 0) s_done = 0;
+  __syncthreads();
+  int nsteps = 0;
+  double beta_prev = 0.0;
+  // First convergence check at step 16; later checks where the residual's
+  // geometric decay since the previous check predicts convergence (at most 8
+  // steps on). Offline study on C3 null items (tools/sim_lanczos.py): 36.0
+  // steps/item vs 37.9 for a fixed 8-step cadence, same number of checks.
+  int next_check = mcap < 16 ? mcap : 16;
+  int prev_j = 0;  // lane 0 of wave 0 only
+  double prev_r = 0.0;
+  const double sqrt_eps = 1.4901161193847656e-08;
+  bool force_next = false;
+  double anorm = 0.0;
+  if (tid == 0) {
+    omg[0] = 1.0;  // omega_{0,0}
+    s_reorth = 0;
+  }
+  for (int j = 0; j < mcap; ++j) {
+    for (int c = tid; c < k; c += BS) Q[(int64_t)j * k + c] = q[c];
+    NR_STAMP(2);  // Lanczos: vector updates / tridiagonal checks
+    const double alpha0 = mv(q, w, q);
+    NR_STAMP(3);  // Lanczos: matvec
+    double nb = three_term<NW>(k, w, q, qprev, alpha0, beta_prev, red);
+    double alpha_j = alpha0;
+    double* om_cur = omg + (j % 3) * (mmax + 1);
+    double* om_prev = omg + ((j + 2) % 3) * (mmax + 1);
+    double* om_next = omg + ((j + 1) % 3) * (mmax + 1);
+    anorm = fmax(anorm, fabs(alpha0) + sqrt(nb) + beta_prev);
+    if (tid == 0) alpha[j] = alpha0;
+    __syncthreads();
+    if (wave == 0) {
+      const double mx = omega_update(alpha, beta, j, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
+      if (lane == 0) s_reorth = force_next || mx > sqrt_eps;
+    }
+    __syncthreads();
+    if (s_reorth) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
+      nb = BF ? reorthogonalise_bf<NW>(Q, k, j + 1, w, h, twork, 5 * mmax, red)  // twork idle until the next check
+              : reorthogonalise_cgs<NW>(Q, k, j + 1, w, h, red);
+      alpha_j += h[j];
+      if (wave == 0) {
+        const double eps = 2.220446049250313e-16;
+        for (int i = lane; i <= j; i += 64) om_next[i] = eps;
+      }
+      force_next = !force_next;
+      if (P.diag && tid == 0) atomicAdd(P.diag + 3, 1);
+    }
+    NR_STAMP(4);  // Lanczos: reorthogonalisation
+    const double beta_j = sqrt(nb);
+    if (tid == 0) {
+      alpha[j] = alpha_j;
+      beta[j] = beta_j;
+    }
+    nsteps = j + 1;
+    __syncthreads();
+    const bool last = (j + 1 == mcap);
+    if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
+      if (wave == 0) {
+        const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane);
+        const double resid = tri_top_resid(alpha, beta, j + 1, theta, beta_j, ty, lane);
+        if (lane == 0) {
+          const double tol = 5e-15 * fabs(theta);
+          const bool conv = resid <= tol;
+          s_done = conv || last || !(beta_j > 1e-300 * fabs(theta));
+          // the Ritz vector's coefficients: inverse iteration (LU), once
+          if (s_done) tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
+          if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
+          int step = 8;
+          if (prev_j > 0 && resid < prev_r && resid > 0.0) {
+            const double rate = log(resid / prev_r) / (double)(j + 1 - prev_j);  // < 0
+            const double need = ceil(log(tol / resid) / rate);
+            step = need < 1.0 ? 1 : (need > 8.0 ? 8 : (int)need);
+          }
+          prev_j = j + 1;
+          prev_r = resid;
+          s_next_check = min(j + 1 + step, mcap);
+        }
+      }
+      __syncthreads();
+      if (s_done) break;
+      next_check = s_next_check;
+    }
+    const double inv = 1.0 / beta_j;
+    for (int c = tid; c < k; c += BS) {
+      qprev[c] = q[c];
+      q[c] = w[c] * inv;
+    }
+    beta_prev = beta_j;
+    __syncthreads();
+  }
+  NR_STAMP(2);
+  if (tid == 0 && P.diag) {
+    atomicAdd(P.diag + 1, 1);
+    atomicAdd(P.diag + 2, nsteps);
+  }
+  // Ritz vector v = Q y, normalised
+  double nv[1] = {0.0};
+  for (int c = tid; c < k; c += BS) {
+    double s = 0.0;
+    for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
+    L.vv[c] = s;
+    nv[0] += s * s;
+  }
+  block_sums<1, NW>(nv, red);
+  {
+    const double inv = 1.0 / sqrt(nv[0]);
+    for (int c = tid; c < k; c += BS) L.vv[c] *= inv;
+  }
+  __syncthreads();
+}
+
+// Node contributions from the Ritz vector (u = X v / sigma):
+//   NC_j = cor(x_j, u) = ((Gv)_j/sigma - S m_j ubar) / sqrt((G_jj - S m_j^2)(1 - S ubar^2)),
+// oriented by sign(cor(rowMeans(X), u)) (src/netStats.cpp:242-247, 279); the
+// result goes to L.w. diag(c) = G_cc; L.colm holds the column means.
+template <int NW, class MV, class DG>
+__device__ __forceinline__ void profile_contrib(const ProfileParams& P, int k, int m, const LzLds& L,
+                                                const double* __restrict__ X, int S, double ones_g_ones,
+                                                MV& mv, DG diag) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x;
+  const double Sd = (double)S;
+  double* vv = L.vv;
+  double* gv = L.gv;
+  double* colm = L.colm;
+  mv(vv, gv, nullptr);
+  // lambda = v.Gv; ubar = mean of u = X v / sigma
+  double a3[2] = {0.0, 0.0};
+  for (int c = tid; c < k; c += BS) {
+    a3[0] += vv[c] * gv[c];
+    a3[1] += colm[c] * vv[c];
+  }
+  block_sums<2, NW>(a3, L.red);
+  const double lambda = a3[0];
+  const double sigma = sqrt(lambda);
+  const double ubar = a3[1] / sigma;
+  const double var_u = 1.0 - Sd * ubar * ubar;  // sum (u - ubar)^2 with |u| = 1
+  // orientation: sign(cor(meanObs, u)) (src/netStats.cpp:242-247); the sign
+  // of the covariance is that of sum_j cov(x_j, u); var(meanObs) * k^2 * (S-1)
+  // = 1'G1 - (sum of all data)^2 / S.
+  double a4[2] = {0.0, 0.0};
+  for (int c = tid; c < k; c += BS) {
+    a4[0] += gv[c] / sigma - Sd * colm[c] * ubar;
+    a4[1] += colm[c];
+  }
+  block_sums<2, NW>(a4, L.red);
+  const double var_mo = ones_g_ones - Sd * a4[1] * a4[1];
+  const bool flip = (a4[0] < 0.0) && (var_mo > 0.0) && (var_u > 0.0);
+  const double sgn = flip ? -1.0 : 1.0;
+  // NC_j = cor(x_j, u) (src/netStats.cpp:279); node order = CSR order
+  for (int c = tid; c < k; c += BS) {
+    const double cov = gv[c] / sigma - Sd * colm[c] * ubar;
+    const double var_x = diag(c) - Sd * colm[c] * colm[c];
+    L.w[c] = sgn * cov / (sqrt(var_x) * sqrt(var_u));
+  }
+  if (P.sp_out) {
+    for (int r = tid; r < S; r += BS) {
+      double s = 0.0;
+      for (int c = 0; c < k; ++c) s += X[(int64_t)L.idx[c] * S + r] * vv[c];
+      P.sp_out[(int64_t)m * S + r] = sgn * s / sigma;
+    }
+  }
+  __syncthreads();
+}
+
+// svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235).
+template <int NW>
+__device__ __forceinline__ void profile_nonfinite(const ProfileParams& P, int k, int m, int S, const LzLds& L) {
+  constexpr int BS = NW * 64;
+  for (int c = threadIdx.x; c < k; c += BS) L.w[c] = nr_nan();
+  if (P.sp_out)
+    for (int r = threadIdx.x; r < S; r += BS) P.sp_out[(int64_t)m * S + r] = nr_nan();
+  __syncthreads();
+}
+
+// ModuleCoherence (src/netStats.cpp:293-305), Correlation / SignAwareMean
+// against the discovery contribution (src/permutations.cpp:99,101); node
+// contributions in L.w.
+template <int NW>
+__device__ __forceinline__ void profile_stats(const ProfileParams& P, int k, int m, int64_t off,
+                                              int64_t p_local, const LzLds& L) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x;
+  const double* w = L.w;
+  double b1[5] = {0, 0, 0, 0, 0};  // nfinite, sum nc^2, ncc, sx, sy
+  for (int c = tid; c < k; c += BS) {
+    const double y = w[c];
+    if (isfinite(y)) { b1[0] += 1.0; b1[1] += y * y; }
+    if (P.disc_nc) {
+      const double xv = P.disc_nc[off + c];
+      if (isfinite(xv) && isfinite(y)) { b1[2] += 1.0; b1[3] += xv; b1[4] += y; }
+    }
+    if (P.nc_out) P.nc_out[off + c] = y;
+  }
+  block_sums<5, NW>(b1, L.red);
+  const double stat_coh = b1[0] >= 1.0 ? b1[1] / b1[0] : nr_nan();
+  double stat_cc = nr_nan(), stat_ac = nr_nan();
+  if (P.disc_nc && P.out) {
+    const double mx = b1[3] / b1[2], my = b1[4] / b1[2];
+    double b2[4] = {0, 0, 0, 0};
+    for (int c = tid; c < k; c += BS) {
+      const double y = w[c], xv = P.disc_nc[off + c];
+      if (isfinite(xv) && isfinite(y)) {
+        const double dx = xv - mx, dy = y - my;
+        b2[0] += dx * dx;
+        b2[1] += dy * dy;
+        b2[2] += dx * dy;
+        b2[3] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
+      }
+    }
+    block_sums<4, NW>(b2, L.red);
+    stat_cc = b1[2] >= 1.0 ? b2[2] / (sqrt(b2[0]) * sqrt(b2[1])) : nr_nan();
+    stat_ac = b1[2] >= 1.0 ? b2[3] / b1[2] : nr_nan();
+  }
+  if (tid == 0) {
+    if (P.out) {
+      double* o = P.out + (int64_t)P.row_of[m] + (int64_t)P.n_rows * (int64_t)P.n_stat * p_local;
+      o[(int64_t)P.n_rows * P.slot_coherence] = na_fill(stat_coh);
+      o[(int64_t)P.n_rows * P.slot_cor_contrib] = na_fill(stat_cc);
+      o[(int64_t)P.n_rows * P.slot_avg_contrib] = na_fill(stat_ac);
+    }
+    if (P.coh_out) P.coh_out[m] = stat_coh;
+  }
+  __syncthreads();
+}
+
+// Next item from the persistent queue: (module m, local permutation, CSR
+// offset, k) and its index set in L.idx. Returns false when drained.
+template <int NW>
+__device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L, int* flags, int& m,
+                                          int64_t& p_local, int64_t& off, int& k) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x;
+  if (tid == 0) flags[0] = atomicAdd(P.queue, 1);
+  __syncthreads();
+  const int item = flags[0];
+  __syncthreads();
+  if (item >= P.n_items) return false;
+  const int64_t mslot = item / P.n_perm;
+  p_local = item - mslot * P.n_perm;
+  m = P.mod_order[mslot];
+  off = P.node_off[m];
+  k = (int)(P.node_off[m + 1] - off);
+  nr_prp_key key;
+  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
+  for (int c = tid; c < k; c += BS) L.idx[c] = node_index(P.src, key, p_local, off + c);
+  if (tid == 0) flags[1] = 0;
+  __syncthreads();
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Scheme 1 (global scratch): G in the workgroup's scratch slot, full (both
+// triangles) or packed symmetric; the Lanczos matvecs stream it from L2 /
+// Infinity Cache. Any module size that fits the LDS vectors.
 // KB > 0 fixes the LDS layout at compile time for modules of at most KB nodes
 // (every carve-out an immediate offset; frees the SGPRs runtime offsets cost).
+// ---------------------------------------------------------------------------
 template <int NW, bool PACKED, int KB>
 __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   constexpr int BS = NW * 64;
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_flags[8];
   const int kmax = KB > 0 ? KB : P.k_max;
   const int mmax = KB > 0 ? (KB < 160 ? KB : 160) : P.m_max;
   const int S = (int)P.n_samples;
-  double* red = reinterpret_cast<double*>(smem);        // 8 * NW
-  double* q = red + 8 * NW;                        // [kmax] current Lanczos vector
-  double* qprev = q + kmax;                              // [kmax] previous Lanczos vector
-  double* w = qprev + kmax;                              // [kmax]
-  double* vv = w + kmax;                                 // [kmax] Ritz vector
-  double* gv = vv + kmax;                                // [kmax] G v
-  double* colm = gv + kmax;                              // [kmax] column means
-  double* part = colm + kmax;                            // [NW * kmax] matvec partials
-  double* upper = part + NW * kmax;                      // [NW * kmax] (packed only)
-  double* alpha = upper + (PACKED ? NW * kmax : 0);      // [mmax]
-  double* beta = alpha + mmax;                           // [mmax]
-  double* h = beta + mmax;                               // [mmax]
-  double* ty = h + mmax;                                 // [mmax]
-  double* twork = ty + mmax;                             // [5 * mmax]
-  double* omg = twork + 5 * mmax;                        // [3 * (mmax + 1)] omega rows
-  uint32_t* idx = reinterpret_cast<uint32_t*>(omg + 3 * (mmax + 1));  // [kmax]
-  __shared__ int s_item;
-  __shared__ int s_flag;
-  __shared__ int s_done;
-  __shared__ int s_reorth;
-  __shared__ int s_next_check;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;   // Gram
+  double* part;
+  const LzLds L = carve_lds<NW>(smem, kmax, mmax, (int64_t)(PACKED ? 2 : 1) * NW * kmax, &part);
+  double* upper = part + NW * kmax;  // packed only
+  const int tid = threadIdx.x;
+  double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;  // Gram
   const int ld = P.ld;
-  double* Q = G + P.gram_doubles;                                   // Lanczos basis
+  double* Q = G + P.gram_doubles;                                  // Lanczos basis
   const double* __restrict__ X = P.data;
   const double Sd = (double)S;
 
-  for (;;) {
-    if (tid == 0) s_item = atomicAdd(P.queue, 1);
-    __syncthreads();
-    const int item = s_item;
-    __syncthreads();
-    if (item >= P.n_items) break;
-
-    const int64_t mslot = item / P.n_perm;
-    const int64_t p_local = item - mslot * P.n_perm;
-    const int m = P.mod_order[mslot];
-    const int64_t off = P.node_off[m];
-    const int k = (int)(P.node_off[m + 1] - off);
-
-    nr_prp_key key;
-    if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
-    for (int c = tid; c < k; c += BS) idx[c] = node_index(P.src, key, p_local, off + c);
-    if (tid == 0) s_flag = 0;
-    __syncthreads();
+  int m, k;
+  int64_t p_local, off;
+  while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
     NR_STAMP(0);  // queue + index derivation
-
     // ---- Gram [X 1]^T [X 1] on the matrix cores ----
     double g1[1] = {0.0};
     int bad = 0;
-    gram_mfma<NW, PACKED>(X, S, idx, k, G, ld, g1[0], bad);
+    gram_mfma<NW, PACKED>(X, S, L.idx, k, G, ld, g1[0], bad);
     const int kc = k + 1;
-    if (bad) atomicOr(&s_flag, 1);
-    block_sums<1, NW>(g1, red);      // barriers also publish G to the whole workgroup
-    const double ones_g_ones = g1[0];
+    if (bad) atomicOr(&s_flags[1], 1);
+    block_sums<1, NW>(g1, L.red);  // barriers also publish G to the whole workgroup
     NR_STAMP(1);  // Gram
-    // svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235)
-    const bool nonfinite = s_flag != 0;
-
-    if (!nonfinite) {
+    if (s_flags[1] == 0) {
       for (int c = tid; c < k; c += BS)
-        colm[c] = (PACKED ? G[pk_at(k, c, kc)] : G[k + (int64_t)c * ld]) / Sd;
-      // ---- Lanczos with full reorthogonalisation (3-term update + one CGS pass) ----
-      const int mcap = k < mmax ? k : mmax;
-      double nq[1] = {0.0};
-      for (int c = tid; c < k; c += BS) {
-        const uint32_t hsh = nr_lowbias32((uint32_t)c * 0x9E3779B9u + 0x1234567u);
-        const double v = 1.0 + 0.01 * ((double)(hsh & 0xFFFF) / 65536.0 - 0.5);
-        q[c] = v;
-        qprev[c] = 0.0;
-        nq[0] += v * v;
-      }
-      block_sums<1, NW>(nq, red);
-      {
-        const double inv = 1.0 / sqrt(nq[0]);
-        for (int c = tid; c < k; c += BS) q[c] *= inv;
-      }
-      if (tid == 0) s_done = 0;
-      __syncthreads();
-      int nsteps = 0;
-      double beta_prev = 0.0;
-      // Convergence of the top Ritz pair is tested at step 16 and every 8 steps
-      // after (each test is a tridiagonal eigen-solve on one wave).
-      // First check at step 16; later checks where the residual's geometric
-      // decay since the previous check predicts convergence (at most 8 steps
-      // on). Offline study on C3 null items (tools/sim_lanczos.py): 36.0
-      // steps/item vs 37.9 for a fixed 8-step cadence, same number of checks.
-      int next_check = mcap < 16 ? mcap : 16;
-      int prev_j = 0;           // lane 0 of wave 0 only
-      double prev_r = 0.0;
-      const double sqrt_eps = 1.4901161193847656e-08;
-      bool force_next = false;
-      double anorm = 0.0;
-      if (tid == 0) {
-        omg[0] = 1.0;                                    // omega_{0,0}
-        s_reorth = 0;
-      }
-      for (int j = 0; j < mcap; ++j) {
-        for (int c = tid; c < k; c += BS) Q[(int64_t)j * k + c] = q[c];
-        NR_STAMP(2);  // Lanczos: vector updates / tridiagonal checks
-        const double alpha0 = PACKED ? packed_matvec<NW>(G, kc, k, q, w, part, upper, kmax, q, red)
-                                     : matvec(G, ld, k, q, w, part, kmax, q, red);
-        NR_STAMP(3);  // Lanczos: matvec
-        double nb = three_term<NW>(k, w, q, qprev, alpha0, beta_prev, red);
-        double alpha_j = alpha0;
-        double* om_cur = omg + (j % 3) * (mmax + 1);
-        double* om_prev = omg + ((j + 2) % 3) * (mmax + 1);
-        double* om_next = omg + ((j + 1) % 3) * (mmax + 1);
-        anorm = fmax(anorm, fabs(alpha0) + sqrt(nb) + beta_prev);
-        if (tid == 0) alpha[j] = alpha0;
-        __syncthreads();
-        if (wave == 0) {
-          const double mx = omega_update(alpha, beta, j, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
-          if (lane == 0) s_reorth = force_next || mx > sqrt_eps;
-        }
-        __syncthreads();
-        if (s_reorth) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
-          nb = PACKED ? reorthogonalise_bf<NW>(Q, k, j + 1, w, h, twork, 5 * mmax, red)  // twork idle until the next check
-                      : reorthogonalise_cgs<NW>(Q, k, j + 1, w, h, red);
-          alpha_j += h[j];
-          if (wave == 0) {
-            const double eps = 2.220446049250313e-16;
-            for (int i = lane; i <= j; i += 64) om_next[i] = eps;
-          }
-          force_next = !force_next;
-          if (P.diag && tid == 0) atomicAdd(P.diag + 3, 1);
-        }
-        NR_STAMP(4);  // Lanczos: reorthogonalisation
-        const double beta_j = sqrt(nb);
-        if (tid == 0) {
-          alpha[j] = alpha_j;
-          beta[j] = beta_j;
-        }
-        nsteps = j + 1;
-        __syncthreads();
-        const bool last = (j + 1 == mcap);
-        if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
-          if (wave == 0) {
-            const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane);
-            if (lane == 0) {
-              tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
-              const double resid = beta_j * fabs(ty[j]);
-              const double tol = 5e-15 * fabs(theta);
-              const bool conv = resid <= tol;
-              s_done = conv || last || !(beta_j > 1e-300 * fabs(theta));
-              if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
-              int step = 8;
-              if (prev_j > 0 && resid < prev_r && resid > 0.0) {
-                const double rate = log(resid / prev_r) / (double)(j + 1 - prev_j);  // < 0
-                const double need = ceil(log(tol / resid) / rate);
-                step = need < 1.0 ? 1 : (need > 8.0 ? 8 : (int)need);
-              }
-              prev_j = j + 1;
-              prev_r = resid;
-              s_next_check = min(j + 1 + step, mcap);
-            }
-          }
-          __syncthreads();
-          if (s_done) break;
-          next_check = s_next_check;
-        }
-        const double inv = 1.0 / beta_j;
-        for (int c = tid; c < k; c += BS) {
-          qprev[c] = q[c];
-          q[c] = w[c] * inv;
-        }
-        beta_prev = beta_j;
-        __syncthreads();
-      }
-      NR_STAMP(2);
-      if (tid == 0 && P.diag) {
-        atomicAdd(P.diag + 1, 1);
-        atomicAdd(P.diag + 2, nsteps);
-      }
-      // Ritz vector v = Q y, normalised, then G v
-      double nv[1] = {0.0};
-      for (int c = tid; c < k; c += BS) {
-        double s = 0.0;
-        for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
-        vv[c] = s;
-        nv[0] += s * s;
-      }
-      block_sums<1, NW>(nv, red);
-      {
-        const double inv = 1.0 / sqrt(nv[0]);
-        for (int c = tid; c < k; c += BS) vv[c] *= inv;
-      }
-      __syncthreads();
-      if (PACKED) packed_matvec<NW>(G, kc, k, vv, gv, part, upper, kmax, nullptr, red);
-      else matvec(G, ld, k, vv, gv, part, kmax, nullptr, red);
-      // lambda = v.Gv; ubar = mean of u = X v / sigma
-      double a3[2] = {0.0, 0.0};
-      for (int c = tid; c < k; c += BS) {
-        a3[0] += vv[c] * gv[c];
-        a3[1] += colm[c] * vv[c];
-      }
-      block_sums<2, NW>(a3, red);
-      const double lambda = a3[0];
-      const double sigma = sqrt(lambda);
-      const double ubar = a3[1] / sigma;
-      const double var_u = 1.0 - Sd * ubar * ubar;  // sum (u - ubar)^2 with |u| = 1
-      // orientation: sign(cor(meanObs, u)) (src/netStats.cpp:242-247); the sign
-      // of the covariance is that of sum_j cov(x_j, u); var(meanObs) * k^2 * (S-1)
-      // = 1'G1 - (sum of all data)^2 / S.
-      double a4[2] = {0.0, 0.0};
-      for (int c = tid; c < k; c += BS) {
-        a4[0] += gv[c] / sigma - Sd * colm[c] * ubar;
-        a4[1] += colm[c];
-      }
-      block_sums<2, NW>(a4, red);
-      const double var_mo = ones_g_ones - Sd * a4[1] * a4[1];
-      const bool flip = (a4[0] < 0.0) && (var_mo > 0.0) && (var_u > 0.0);
-      const double sgn = flip ? -1.0 : 1.0;
-      // NC_j = cor(x_j, u) (src/netStats.cpp:279); node order = CSR order
-      for (int c = tid; c < k; c += BS) {
-        const double gjj = PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
-        const double cov = gv[c] / sigma - Sd * colm[c] * ubar;
-        const double var_x = gjj - Sd * colm[c] * colm[c];
-        w[c] = sgn * cov / (sqrt(var_x) * sqrt(var_u));
-      }
-      if (P.sp_out) {
-        for (int r = tid; r < S; r += BS) {
-          double s = 0.0;
-          for (int c = 0; c < k; ++c) s += X[(int64_t)idx[c] * S + r] * vv[c];
-          P.sp_out[(int64_t)m * S + r] = sgn * s / sigma;
-        }
-      }
-      __syncthreads();
+        L.colm[c] = (PACKED ? G[pk_at(k, c, kc)] : G[k + (int64_t)c * ld]) / Sd;
+      auto mv = [&](const double* x, double* out, const double* y) -> double {
+        return PACKED ? packed_matvec<NW>(G, kc, k, x, out, part, upper, kmax, y, L.red)
+                      : matvec(G, ld, k, x, out, part, kmax, y, L.red);
+      };
+      lanczos_ritz<NW, PACKED>(P, k, L, s_flags, Q, mv, t_mark);
+      profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) {
+        return PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
+      });
     } else {
-      for (int c = tid; c < k; c += BS) w[c] = nr_nan();
-      if (P.sp_out)
-        for (int r = tid; r < S; r += BS) P.sp_out[(int64_t)m * S + r] = nr_nan();
-      __syncthreads();
+      profile_nonfinite<NW>(P, k, m, S, L);
     }
-
-    // ModuleCoherence (src/netStats.cpp:293-305), Correlation / SignAwareMean
-    // against the discovery contribution (src/permutations.cpp:99,101).
-    double b1[5] = {0, 0, 0, 0, 0};  // nfinite, sum nc^2, ncc, sx, sy
-    for (int c = tid; c < k; c += BS) {
-      const double y = w[c];
-      if (isfinite(y)) { b1[0] += 1.0; b1[1] += y * y; }
-      if (P.disc_nc) {
-        const double xv = P.disc_nc[off + c];
-        if (isfinite(xv) && isfinite(y)) { b1[2] += 1.0; b1[3] += xv; b1[4] += y; }
-      }
-      if (P.nc_out) P.nc_out[off + c] = y;
-    }
-    block_sums<5, NW>(b1, red);
-    const double stat_coh = b1[0] >= 1.0 ? b1[1] / b1[0] : nr_nan();
-    double stat_cc = nr_nan(), stat_ac = nr_nan();
-    if (P.disc_nc && P.out) {
-      const double mx = b1[3] / b1[2], my = b1[4] / b1[2];
-      double b2[4] = {0, 0, 0, 0};
-      for (int c = tid; c < k; c += BS) {
-        const double y = w[c], xv = P.disc_nc[off + c];
-        if (isfinite(xv) && isfinite(y)) {
-          const double dx = xv - mx, dy = y - my;
-          b2[0] += dx * dx;
-          b2[1] += dy * dy;
-          b2[2] += dx * dy;
-          b2[3] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
-        }
-      }
-      block_sums<4, NW>(b2, red);
-      stat_cc = b1[2] >= 1.0 ? b2[2] / (sqrt(b2[0]) * sqrt(b2[1])) : nr_nan();
-      stat_ac = b1[2] >= 1.0 ? b2[3] / b1[2] : nr_nan();
-    }
-    if (tid == 0) {
-      if (P.out) {
-        double* o = P.out + (int64_t)P.row_of[m] + (int64_t)P.n_rows * (int64_t)P.n_stat * p_local;
-        o[(int64_t)P.n_rows * P.slot_coherence] = na_fill(stat_coh);
-        o[(int64_t)P.n_rows * P.slot_cor_contrib] = na_fill(stat_cc);
-        o[(int64_t)P.n_rows * P.slot_avg_contrib] = na_fill(stat_ac);
-      }
-      if (P.coh_out) P.coh_out[m] = stat_coh;
-    }
-    __syncthreads();
+    profile_stats<NW>(P, k, m, off, p_local, L);
     NR_STAMP(5);  // Ritz vector, contributions, statistics
   }
 }
@@ -1130,6 +1268,394 @@ template <int KB, int OCC>
 __global__ void __launch_bounds__(NR_BS, OCC)
 module_profile_packed4_kernel(ProfileParams P) {
   profile_body<NR_WAVES, true, KB>(P);
+}
+
+// ---------------------------------------------------------------------------
+// Scheme 2 (register-resident, the default for modules of <= 16*RG_TMAX - 1
+// nodes): one 8-wave workgroup per CU. G = [X 1]^T [X 1] is cut into 16 x 16
+// tiles over the upper triangle (T = ceil((k+1)/16) tiles a side, row-major
+// tile ids 0..T(T+1)/2-1); wave w computes the contiguous id range
+// [w*nt/8, (w+1)*nt/8) with v_mfma_f64_16x16x4_f64 and KEEPS the
+// accumulators: its first RG_RT tiles stay in VGPRs, the rest (<= RG_LT) go to
+// an LDS slot in the same lane layout. Those registers are the Lanczos
+// operator: no byte of G ever goes to memory, and a matvec is 8 FMAs per
+// lane per tile plus register butterflies:
+//   type 1 (all tiles):  w_I += G_IJ x_J, lane-local over a run of equal I,
+//                        reduced over the 16 columns by DPP at the run end;
+//   type 2 (I < J):      w_J += G_IJ^T x_I, reduced over the 4 row groups by
+//                        permlane32/16 swaps for 4 tiles at once.
+// Row partials go to per-wave rows (rowp) and column partials to per-tile
+// slots (colp); one pass sums them in a fixed order (deterministic).
+// ---------------------------------------------------------------------------
+constexpr int RG_NW = 8;     // waves per workgroup
+constexpr int RG_RT = 20;    // register tiles per wave (80 doubles of accumulators per lane)
+constexpr int RG_LT = 4;     // LDS tiles per wave
+constexpr int RG_TMAX = 19;  // tiles a side: k + 1 <= 304
+constexpr int RG_KP = 16 * RG_TMAX;
+constexpr int RG_NTMAX = RG_TMAX * (RG_TMAX + 1) / 2;
+static_assert((RG_RT + RG_LT) % 4 == 0, "tile groups of four");
+static_assert(RG_NW * (RG_RT + RG_LT) >= RG_NTMAX, "tile capacity");
+static_assert((RG_NTMAX + RG_NW - 1) / RG_NW <= RG_RT + RG_LT, "per-wave tile capacity");
+static_assert(RG_NW * RG_KP + RG_NTMAX * 16 >= RG_KP * 18, "row slab fits the rowp/colp region");
+
+// Rows s .. s+3 of Gram column c: a data column (colofs[c] = idx * S), the
+// virtual all-ones column (-1) or zero padding (-2); rows >= S are zero.
+// Branch-free: every lane loads from a valid address (row clamped, padding
+// columns read column 0) and masks the value afterwards.
+__device__ __forceinline__ void rg_load4(const double* __restrict__ X, int o, int s, int S,
+                                         double (&v)[4]) {
+  const bool data = o >= 0;
+  const double fill = o == -1 ? 1.0 : 0.0;
+  const double* col = X + (data ? o : 0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int r = s + t;
+    const double x = col[r < S ? r : S - 1];
+    v[t] = r < S ? (data ? x : fill) : 0.0;
+  }
+}
+
+// Sum of a[r] over lane bits 0..3 (the 16 columns of a tile); lanes with
+// (lane & 3) == 0 end with the total of row group r = 2*b3 + b2, i.e. tile
+// row (lane >> 4) + 4r.
+__device__ __forceinline__ double rg_row_reduce(const double (&a)[4], int lane) {
+  const bool b3 = lane & 8, b2 = lane & 4;
+  const double v0 = (b3 ? a[2] : a[0]) + nr_dpp<NR_DPP_ROR8>(b3 ? a[0] : a[2]);
+  const double v1 = (b3 ? a[3] : a[1]) + nr_dpp<NR_DPP_ROR8>(b3 ? a[1] : a[3]);
+  double v = (b2 ? v1 : v0) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? v0 : v1);
+  v += nr_dpp<NR_DPP_XOR2>(v);
+  v += nr_dpp<NR_DPP_XOR1>(v);
+  return v;
+}
+
+// Per-wave tile range of the register scheme: ids [t0, t0 + n); the first
+// nreg = min(n, RG_RT) stay in registers, the remaining nl go to LDS.
+struct RgTiles {
+  int T, nt, t0, n, nreg, nl;  // tiles a side, tiles, this wave's range and split
+  int I0, J0;                  // coordinates of tile t0
+  int Il, Jl;                  // coordinates of tile t0 + nreg (first LDS tile)
+};
+
+// (I, J) of tile id t (t == T(T+1)/2, one past the end, gives (T, T)).
+__device__ __forceinline__ void rg_coords(int T, int t, int& I, int& J) {
+  I = 0;
+  while (I < T && t >= T - I) { t -= T - I; ++I; }
+  J = I + t;
+}
+
+__device__ __forceinline__ RgTiles rg_tiles(int k, int wave) {
+  RgTiles R;
+  R.T = (k + 1 + 15) / 16;
+  R.nt = R.T * (R.T + 1) / 2;
+  R.t0 = wave * R.nt / RG_NW;
+  R.n = (wave + 1) * R.nt / RG_NW - R.t0;
+  R.nreg = R.n < RG_RT ? R.n : RG_RT;
+  R.nl = R.n - R.nreg;
+  rg_coords(R.T, R.t0, R.I0, R.J0);
+  rg_coords(R.T, R.t0 + R.nreg, R.Il, R.Jl);
+  return R;
+}
+
+// Gram tiles acc[t] = G tile (I_t, J_t), t < cnt, the tiles following
+// (I0, J0) in row-major upper-triangle order. The rows go through LDS in
+// slabs of 16: all 512 threads stage rows s0..s0+15 of every column of
+// [X 1] (8 threads x 16 B per column, coalesced; non-finite check here, once
+// per value) into `slab` (column stride RG_SLD doubles: conflict-free
+// ds_read_b128), while the previous slab feeds the MFMAs (register staging,
+// one slab buffer, two barriers per slab). Each lane then feeds rows
+// 4*kk .. 4*kk+3 of its column to 4 MFMAs (the K order permuted identically
+// for both operands); the J block of the next tile is read one tile ahead;
+// a run of equal I starts at its diagonal tile, whose J block is the I block.
+// Every thread of the workgroup must call this (barriers), cnt may be 0.
+constexpr int RG_SLD = 18;
+template <int NTW>
+__device__ __forceinline__ void rg_gram(nr_f64x4 (&acc)[NTW], int T, int I0, int J0, int cnt,
+                                        const double* __restrict__ X, int S, const int* colofs, double* slab,
+                                        int& bad) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int kp = 16 * T;
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) acc[t] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+  constexpr int NR = (RG_KP + 63) / 64;  // staging rounds of 64 columns
+  const int part = tid & 7, cbase = tid >> 3;
+  int o[NR];
+#pragma unroll
+  for (int u = 0; u < NR; ++u) {
+    const int c = cbase + 64 * u;
+    o[u] = c < kp ? colofs[c] : -3;  // -3: no such column this item
+  }
+  double st[NR][2];
+  auto stage_load = [&](int s0) {
+    const int r = s0 + 2 * part;
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const bool data = o[u] >= 0;
+      const double* col = X + (data ? o[u] : 0);
+      const double x0 = col[r < S ? r : S - 1];
+      const double x1 = col[r + 1 < S ? r + 1 : S - 1];
+      const double f = o[u] == -1 ? 1.0 : 0.0;
+      st[u][0] = r < S ? (data ? x0 : f) : 0.0;
+      st[u][1] = r + 1 < S ? (data ? x1 : f) : 0.0;
+      bad |= (int)!isfinite(st[u][0]) | (int)!isfinite(st[u][1]);
+    }
+  };
+  auto blk = [&](int b, double (&v)[4]) {
+    const double* p = slab + (b * 16 + i16) * RG_SLD + 4 * kk;
+    const double2 lo = *reinterpret_cast<const double2*>(p);
+    const double2 hi = *reinterpret_cast<const double2*>(p + 2);
+    v[0] = lo.x;
+    v[1] = lo.y;
+    v[2] = hi.x;
+    v[3] = hi.y;
+  };
+  stage_load(0);
+  for (int s0 = 0; s0 < S; s0 += 16) {
+    __syncthreads();  // the previous slab is consumed
+#pragma unroll
+    for (int u = 0; u < NR; ++u)
+      if (o[u] != -3)
+        *reinterpret_cast<double2*>(slab + (cbase + 64 * u) * RG_SLD + 2 * part) = make_double2(st[u][0], st[u][1]);
+    __syncthreads();
+    if (s0 + 16 < S) stage_load(s0 + 16);  // in flight during the MFMAs below
+    if (cnt > 0) {
+      int I = I0, J = J0;
+      double a[4], b[4], bn[4];
+      if (I0 != J0) blk(I0, a);
+      blk(J0, b);
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) {
+        if (t < cnt) {
+          int In = I, Jn = J + 1;
+          if (Jn == T) {
+            ++In;
+            Jn = In;
+          }
+          if (t + 1 < cnt) blk(Jn, bn);
+          if (J == I) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = b[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc[t], 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) b[q] = bn[q];
+          I = In;
+          J = Jn;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+}
+
+// Gram epilogue over cnt tiles from (I, J): 1'G1 over the X block (weight 2
+// off the diagonal), the diagonal, the column means (column k holds the
+// column sums), and -- for LDS tiles -- the store into the wave's slot.
+template <int NTW>
+__device__ __forceinline__ void rg_epilogue(const nr_f64x4 (&acc)[NTW], int T, int I, int J, int cnt, int k,
+                                            double Sd, double& g1, double* gdiag, double* colm, double* lt) {
+  const int lane = threadIdx.x & 63;
+  const int i16 = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    if (t < cnt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = I * 16 + kk + 4 * r, gj = J * 16 + i16;
+        const double v = acc[t][r];
+        if (gi < k && gj < k) g1 += (I == J ? 1.0 : 2.0) * v;
+        if (gi == gj) gdiag[gi] = v;
+        if (gj == k) colm[gi] = v / Sd;  // column sums -> means (rows gi <= k)
+        if (lt) lt[t * 256 + r * 64 + lane] = v;
+      }
+      if (++J == T) {
+        ++I;
+        J = I;
+      }
+    }
+  }
+}
+
+template <int NTW>
+struct RgMatvec {
+  nr_f64x4 (&acc)[RG_RT];
+  const RgTiles& R;
+  const double* ltile;  // this wave's LDS tiles [RG_LT][4][64]
+  double* rowp;         // [RG_NW][RG_KP]
+  double* colp;         // [RG_NTMAX][16]
+  double* red;
+  int k;
+
+  // out = G x for rows < k; returns y . out (block-wide) when y != NULL.
+  // x must be zero from k to 16*T.
+  __device__ __forceinline__ double operator()(const double* x, double* out, const double* y) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i16 = lane & 15, kk = lane >> 4;
+    const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
+    const int rrow = kk + 4 * (2 * ((lane >> 3) & 1) + ((lane >> 2) & 1));
+    // Opaque per call: otherwise the per-tile address arithmetic is hoisted
+    // out of the Lanczos loop and pins dozens of VGPRs next to the tiles.
+    int I = R.I0, J = R.J0, n = R.n, t0 = R.t0, T = R.T;
+    asm volatile("" : "+s"(I), "+s"(J), "+s"(n), "+s"(t0), "+s"(T));
+    double ra[4] = {0.0, 0.0, 0.0, 0.0};
+    double xi[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xi[r] = x[I * 16 + kk + 4 * r];
+    double cx[4];
+    int cid[4];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+      if (t < n) {
+        double g[4];
+        if (t < RG_RT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g[r] = acc[t][r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g[r] = ltile[(t - RG_RT) * 256 + r * 64 + lane];
+        }
+        const double xj = x[J * 16 + i16];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ra[r] = fma(g[r], xj, ra[r]);
+        if (I != J) {
+          double c = 0.0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) c = fma(g[r], xi[r], c);
+          cx[t & 3] = c;
+          cid[t & 3] = t0 + t;
+        } else {
+          cx[t & 3] = 0.0;
+          cid[t & 3] = -1;
+        }
+        if (++J == T || t + 1 == n) {  // end of a run of equal I
+          const double v = rg_row_reduce(ra, lane);
+          if ((lane & 3) == 0) rowp[wave * RG_KP + I * 16 + rrow] = v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ra[r] = 0.0;
+          if (J == T) {
+            ++I;
+            J = I;
+            if (t + 1 < n) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) xi[r] = x[I * 16 + kk + 4 * r];
+            }
+          }
+        }
+      } else {
+        cx[t & 3] = 0.0;
+        cid[t & 3] = -1;
+      }
+      if ((t & 3) == 3 && t - 3 < n) {
+        const double a0 = nr_swap32_sum(cx[0], cx[1]);
+        const double a1 = nr_swap32_sum(cx[2], cx[3]);
+        const double v = nr_swap16_sum(a0, a1);
+        const int sl = 2 * b4 + b5;
+        const int id = sl == 0 ? cid[0] : sl == 1 ? cid[1] : sl == 2 ? cid[2] : cid[3];
+        if (id >= 0) colp[id * 16 + i16] = v;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    // out_r = sum_w rowp[w][r] + sum_{I < J(r)} colp[id(I, J(r))][r mod 16];
+    // rowp is zeroed as it is consumed (only runs write it).
+    double d[1] = {0.0};
+    const int kp = 16 * R.T;
+    for (int rr = threadIdx.x; rr < kp; rr += RG_NW * 64) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < RG_NW; ++w) {
+        s += rowp[w * RG_KP + rr];
+        rowp[w * RG_KP + rr] = 0.0;
+      }
+      const int Jr = rr >> 4, c = rr & 15;
+      int id = Jr;  // id(0, Jr)
+      for (int Ii = 0; Ii < Jr; ++Ii) {
+        s += colp[id * 16 + c];
+        id += R.T - Ii - 1;
+      }
+      if (rr < k) {
+        out[rr] = s;
+        if (y) d[0] += y[rr] * s;
+      }
+    }
+    block_sums<1, RG_NW>(d, red);
+    return d[0];
+  }
+};
+
+size_t reg_kernel_lds(int m_max);
+
+__global__ void __launch_bounds__(RG_NW * 64, 2)
+module_profile_reg_kernel(ProfileParams P) {
+  constexpr int NW = RG_NW, BS = NW * 64, NTW = RG_RT + RG_LT;
+  uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_flags[8];
+  const int mmax = RG_KP < 160 ? RG_KP : 160;
+  const int S = (int)P.n_samples;
+  double* ex;
+  const int64_t extra = (int64_t)NW * RG_KP + (int64_t)RG_NTMAX * 16 + RG_KP + (int64_t)NW * RG_LT * 256 +
+                        RG_KP / 2;
+  const LzLds L = carve_lds<NW>(smem, RG_KP, mmax, extra, &ex);
+  double* rowp = ex;                              // [NW][KP]
+  double* colp = rowp + NW * RG_KP;               // [NTMAX][16]
+  double* gdiag = colp + RG_NTMAX * 16;           // [KP]
+  double* ltiles = gdiag + RG_KP;                 // [NW][LT][256]
+  int* colofs = reinterpret_cast<int*>(ltiles + NW * RG_LT * 256);  // [KP]
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* Q = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;  // Lanczos basis
+  const double* __restrict__ X = P.data;
+  const double Sd = (double)S;
+  double* ltile = ltiles + wave * RG_LT * 256;
+  for (int i = tid; i < NW * RG_KP; i += BS) rowp[i] = 0.0;
+
+  int m, k;
+  int64_t p_local, off;
+  while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
+    NR_STAMP(0);  // queue + index derivation
+    const RgTiles R = rg_tiles(k, wave);
+    const int kp = 16 * R.T;
+    for (int c = tid; c < kp; c += BS) {
+      colofs[c] = c < k ? (int)L.idx[c] * S : (c == k ? -1 : -2);
+      if (c >= k) {  // the Lanczos inputs are zero beyond k
+        L.q[c] = 0.0;
+        L.vv[c] = 0.0;
+      }
+    }
+    __syncthreads();
+    NR_STAMP(6);  // tile ranges, column offsets
+    // ---- Gram tiles on the matrix cores, kept where they were computed ----
+    int bad = 0;
+    double g1[1] = {0.0};
+    // The row slabs are staged in the rowp/colp region (idle until the
+    // Lanczos matvecs); pass 1 only where some wave overflows into LDS.
+    double* slab = rowp;
+    if ((R.nt + NW - 1) / NW > RG_RT) {  // pass 1: the tiles that overflow into the LDS slots
+      nr_f64x4 accl[RG_LT];
+      rg_gram<RG_LT>(accl, R.T, R.Il, R.Jl, R.nl, X, S, colofs, slab, bad);
+      rg_epilogue<RG_LT>(accl, R.T, R.Il, R.Jl, R.nl, k, Sd, g1[0], gdiag, L.colm, ltile);
+    }
+    nr_f64x4 acc[RG_RT];  // pass 2: the register tiles (live until the item ends)
+    rg_gram<RG_RT>(acc, R.T, R.I0, R.J0, R.nreg, X, S, colofs, slab, bad);
+    rg_epilogue<RG_RT>(acc, R.T, R.I0, R.J0, R.nreg, k, Sd, g1[0], gdiag, L.colm, nullptr);
+    if (bad) atomicOr(&s_flags[1], 1);
+    __syncthreads();  // slab reads done before rowp is cleared
+    for (int i = tid; i < NW * RG_KP; i += BS) rowp[i] = 0.0;
+    block_sums<1, NW>(g1, L.red);  // barriers also publish gdiag, colm and the LDS tiles
+    NR_STAMP(1);  // Gram
+    if (s_flags[1] == 0) {
+      RgMatvec<NTW> mv{acc, R, ltile, rowp, colp, L.red, k};
+      lanczos_ritz<NW, false>(P, k, L, s_flags, Q, mv, t_mark);
+      profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) { return gdiag[c]; });
+    } else {
+      profile_nonfinite<NW>(P, k, m, S, L);
+    }
+    profile_stats<NW>(P, k, m, off, p_local, L);
+    NR_STAMP(5);  // Ritz vector, contributions, statistics
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1225,9 +1751,20 @@ size_t net_kernel_lds(int k_max) {
 // Compile-time module-size bucket of the packed kernel (0 = runtime layout).
 int packed_bucket(int k_max) { return k_max <= 320 ? 320 : 0; }
 
-// variant: 0 full Gram (4 waves), 1 packed (8 waves), 2 packed (4 waves)
+size_t reg_kernel_lds(int m_max) {
+  (void)m_max;  // compile-time layout (mmax = 160)
+  const size_t mmax = RG_KP < 160 ? RG_KP : 160;
+  const size_t extra = (size_t)RG_NW * RG_KP + (size_t)RG_NTMAX * 16 + RG_KP + (size_t)RG_NW * RG_LT * 256 + RG_KP / 2;
+  return sizeof(double) * (8 * RG_NW + 6 * (size_t)RG_KP + extra + 12 * mmax + 3) + sizeof(uint32_t) * RG_KP;
+}
+
+int reg_kernel_k_max() { return RG_KP - 1; }
+
+// variant: 0 full Gram (4 waves), 1 packed (8 waves), 2 packed (4 waves),
+// 3 register-resident (8 waves, one workgroup per CU)
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
   (void)n_samples;
+  if (variant == 3) return reg_kernel_lds(m_max);
   const bool packed = variant != 0;
   const int nw = variant == 1 ? 8 : NR_WAVES;
   if (packed && packed_bucket(k_max) > 0) {
@@ -1250,6 +1787,10 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
   const dim3 g((unsigned)n_slots), b(512), b4(NR_BS);
   const bool b320 = packed_bucket(P.k_max) == 320;
   const bool packed = variant == 1;
+  if (variant == 3) {
+    hipLaunchKernelGGL(module_profile_reg_kernel, g, dim3(RG_NW * 64), lds, st, P);
+    return hipGetLastError();
+  }
   if (variant == 2) {
     if (b320 && wg_per_cu >= 3)
       hipLaunchKernelGGL((module_profile_packed4_kernel<320, 3>), g, b4, lds, st, P);

@@ -208,8 +208,8 @@ class Engine:
     def stamps(self):
         out = (C.c_uint64 * 8)()
         self._check(self._lib.nr_get_stamps(self._h, out))
-        names = ["index", "gram", "lanczos_vec", "lanczos_matvec", "reorth", "tail"]
-        return dict(zip(names, list(out)[:6]))
+        names = ["index", "gram", "lanczos_vec", "lanczos_matvec", "reorth", "tail", "setup", "spare"]
+        return dict(zip(names, list(out)))
 
     def reset_timing(self):
         self._check(self._lib.nr_reset_timing(self._h))

@@ -300,3 +300,16 @@ def test_netprops_one_node_and_absent_modules(bundled):
     na = np.uint64(0x7FF00000000007A2)
     assert np.float64(got["solo"]["avgWeight"]).view(np.uint64) != na
     assert np.float64(got["ghost"]["avgWeight"]).view(np.uint64) == na
+
+
+@pytest.mark.parametrize("variant", ["reg", "packed4", "packed", "full"])
+def test_profile_kernel_variants(variant, monkeypatch, bundled, bundled_expected):
+    """Every summary-profile Gram scheme (NETREP_PROFILE_VARIANT) against the
+    oracles: register-resident tiles, packed symmetric (4 and 8 waves), full
+    storage. C3-like module sizes vs the C++ LAPACK restatement, the bundled
+    data vs the golden cube, and the non-finite (svd failure) path."""
+    monkeypatch.setenv("NETREP_PROFILE_VARIANT", variant)
+    test_large_modules_vs_cpp_oracle(11)
+    test_bundled_observed_and_nulls_explicit_pi(bundled, bundled_expected, True)
+    test_constant_column_gives_na()
+    test_engine_synthetic_vs_oracle(True)
