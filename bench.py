@@ -215,16 +215,20 @@ def main():
     if rank == 0:
         value = total_perms / elapsed
         # dominant kernel + roofline (per launch = one batch of B permutations)
-        kernels = {
-            "module_net_kernel": {"bound": "hbm", "avg_ms": ms0 / max(l0, 1), "launches": l0,
-                                  "achieved": net_b * B / (ms0 / max(l0, 1) / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
-                                  "unit": "GB/s"},
-        }
+        kernels = {}
+        fused = meta["with_data"] and l0 == 0   # network statistics computed inside the profile kernel
+        if l0 > 0:
+            kernels["module_net_kernel"] = {
+                "bound": "hbm", "avg_ms": ms0 / l0, "launches": l0,
+                "achieved": net_b * B / (ms0 / l0 / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
         if meta["with_data"]:
+            t1 = ms1 / max(l1, 1) / 1e3
             kernels["module_profile_kernel"] = {
                 "bound": "mfma", "avg_ms": ms1 / max(l1, 1), "launches": l1,
-                "achieved": prof_f * B / (ms1 / max(l1, 1) / 1e3) / 1e12, "peak": FP64_MFMA_PEAK_TFS,
-                "unit": "TFLOP/s"}
+                "achieved": prof_f * B / t1 / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "fused_network_statistics": fused,
+                # algorithmic HBM bytes the launch moves (gathers + data columns) per its duration
+                "hbm_achieved_GBps": ((net_b if fused else 0.0) + prof_b) * B / t1 / 1e9}
         for kv in kernels.values():
             kv["frac"] = kv["achieved"] / kv["peak"]
         dom_name = max(kernels, key=lambda n: kernels[n]["avg_ms"])

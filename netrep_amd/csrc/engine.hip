@@ -79,6 +79,7 @@ struct nr_ctx {
   size_t stage_cap = 0;
   uint32_t* d_pi = nullptr;
   size_t pi_cap = 0;
+  bool fuse_net = true;      // network statistics fused into the profile kernel (NETREP_FUSE)
   double* d_scratch = nullptr;
   size_t scratch_cap = 0;
   int* d_counters = nullptr;  // [0] queue head, [1..4] lanczos diagnostics, [5] flag
@@ -291,15 +292,22 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   np.slot_cor_degree = data ? 3 : 2;
   np.slot_avg_cor = data ? 5 : 3;
   np.out = d_out;
-  const bool fork = data && ctx->concurrent;
+  // Default with data: the network statistics run inside the summary-profile
+  // kernel (fused per item), so their HBM-bound gathers overlap the matrix and
+  // Lanczos work of the co-resident workgroups. NETREP_FUSE=0 launches them
+  // as their own kernel (optionally on the side stream, NETREP_CONCURRENT=1).
+  const bool fuse = data && ctx->fuse_net;
+  const bool fork = data && !fuse && ctx->concurrent;
   hipStream_t net_stream = fork ? ctx->side : ctx->stream;
   if (fork) {
     NR_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
     NR_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   }
-  timer_begin(ctx, 0, net_stream);
-  NR_HIP(ctx, nr::launch_net(np, n_items, net_stream));
-  timer_end(ctx, 0, n_items, net_stream);
+  if (!fuse) {
+    timer_begin(ctx, 0, net_stream);
+    NR_HIP(ctx, nr::launch_net(np, n_items, net_stream));
+    timer_end(ctx, 0, n_items, net_stream);
+  }
 
   if (data) {
     ProfilePlan plan;
@@ -331,6 +339,8 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.queue = ctx->d_counters;
     pp.diag = ctx->d_counters + 1;
     pp.stamps = ctx->d_stamps;
+    pp.fuse_net = fuse ? 1 : 0;
+    pp.net = np;
     timer_begin(ctx, 1, ctx->stream);
     NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, ctx->stream));
     timer_end(ctx, 1, n_items, ctx->stream);
@@ -447,6 +457,7 @@ int nr_ctx_create(int device, nr_ctx** out) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (const char* c = std::getenv("NETREP_CONCURRENT")) ctx->concurrent = std::atoi(c) != 0;
+  if (const char* f = std::getenv("NETREP_FUSE")) ctx->fuse_net = std::atoi(f) != 0;
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, 16 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, 16 * sizeof(int));

@@ -65,6 +65,8 @@ struct ProfileParams {
   int* queue;                  // work-queue head, zeroed before launch
   int* diag;                   // [0] Lanczos step-cap hits, [1] items, [2] Lanczos steps, [3] reorthogonalisations
   unsigned long long* stamps;  // [8] per-phase shader cycles (diagnostics; NULL = off)
+  int fuse_net;                // 1: each item also computes the network statistics (net)
+  NetParams net;
 };
 
 size_t net_kernel_lds(int k_max);

@@ -94,34 +94,27 @@ __device__ __forceinline__ void decode_pair(int64_t v, int64_t k, int64_t& jj, i
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 1: module network statistics. One workgroup per item.
+// Module network statistics of one item (p, m): avg.weight, cor.cor,
+// cor.degree, avg.cor (CorrVector + WeightedDegree gathers, src/netStats.cpp:
+// 124-204; src/permutations.cpp:75-97). Run by a whole NW-wave workgroup,
+// either as its own kernel (one workgroup per item) or fused into the
+// summary-profile bodies, where its HBM-bound gather overlaps the matrix /
+// latency-bound work of the co-resident workgroups. idx[0..k) (LDS) holds the
+// item's test columns; wd is NW x wd_stride doubles of LDS scratch; red holds
+// 8 * NW doubles.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(NR_BS)
-module_net_kernel(NetParams P) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* red = reinterpret_cast<double*>(smem);                    // 8 * NR_WAVES
-  double* wd = red + 8 * NR_WAVES;                                  // [NR_WAVES][k_max]
-  uint32_t* idx = reinterpret_cast<uint32_t*>(wd + NR_WAVES * P.k_max);  // [k]
+template <int NW>
+__device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_local, int64_t off, int64_t k,
+                                         const uint32_t* idx, double* red, double* wd, int wd_stride) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x;
   // Each wave accumulates the weighted degrees into its own copy: the pair ->
   // (wave, lane, iteration) assignment is fixed, so the sums are bitwise
   // reproducible; the copies are added in wave order afterwards.
-  double* wdw = wd + (threadIdx.x >> 6) * P.k_max;
-
-  const int64_t item = blockIdx.x;
-  const int64_t mslot = item / P.n_perm;
-  const int64_t p_local = item - mslot * P.n_perm;
-  const int m = P.mod_order[mslot];
-  const int64_t off = P.node_off[m];
-  const int64_t k = P.node_off[m + 1] - off;
-  const int tid = threadIdx.x;
-
-  nr_prp_key key;
-  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
-
-  for (int64_t c = tid; c < k; c += NR_BS) {
-    idx[c] = node_index(P.src, key, p_local, off + c);
+  double* wdw = wd + (threadIdx.x >> 6) * wd_stride;
+  for (int64_t c = tid; c < k; c += BS) {
 #pragma unroll
-    for (int w = 0; w < NR_WAVES; ++w) wd[w * P.k_max + c] = 0.0;
+    for (int w = 0; w < NW; ++w) wd[w * wd_stride + c] = 0.0;
   }
   __syncthreads();
 
@@ -135,21 +128,21 @@ module_net_kernel(NetParams P) {
   const double ys = npairs > 0 ? pairs[(int64_t)idx[1] + (int64_t)idx[0] * n].x : 0.0;
 
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // n, sx, sy, sxx, syy, sxy, s(sign(x) y)
-  constexpr int U = 4;
-  for (int64_t v0 = tid; v0 < npairs; v0 += (int64_t)NR_BS * U) {
+  constexpr int U = 8;  // pairs in flight per thread (random 16-byte gathers)
+  for (int64_t v0 = tid; v0 < npairs; v0 += (int64_t)BS * U) {
     double2 e[U];
     double e2[U];
     double x[U];
-    int64_t jjs[U], iis[U];
+    int jjs[U], iis[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t v = v0 + (int64_t)u * NR_BS;
+      const int64_t v = v0 + (int64_t)u * BS;
       jjs[u] = -1;
       if (v < npairs) {
         int64_t jj, ii;
         decode_pair(v, k, jj, ii);
-        jjs[u] = jj;
-        iis[u] = ii;
+        jjs[u] = (int)jj;
+        iis[u] = (int)ii;
         const int64_t r = idx[ii], c = idx[jj];
         e[u] = pairs[r + c * n];                      // corr(idx[ii], idx[jj]), net(idx[ii], idx[jj])
         e2[u] = P.symmetric ? e[u].y : pairs[c + r * n].y;  // net(idx[jj], idx[ii])
@@ -160,7 +153,7 @@ module_net_kernel(NetParams P) {
     for (int u = 0; u < U; ++u) {
       if (jjs[u] < 0) continue;
       const double y = e[u].x;
-      if (P.cv_out) P.cv_out[cvo + v0 + (int64_t)u * NR_BS] = y;
+      if (P.cv_out) P.cv_out[cvo + v0 + (int64_t)u * BS] = y;
       atomicAdd(&wdw[jjs[u]], fabs(e[u].y));    // column idx[jj] gains row idx[ii]
       atomicAdd(&wdw[iis[u]], fabs(e2[u]));     // column idx[ii] gains row idx[jj]
       const double xv = x[u];
@@ -176,11 +169,11 @@ module_net_kernel(NetParams P) {
       }
     }
   }
-  block_sums<7>(acc, red);
-  for (int64_t c = tid; c < k; c += NR_BS) {
+  block_sums<7, NW>(acc, red);
+  for (int64_t c = tid; c < k; c += BS) {
     double s = wd[c];
 #pragma unroll
-    for (int w = 1; w < NR_WAVES; ++w) s += wd[w * P.k_max + c];
+    for (int w = 1; w < NW; ++w) s += wd[w * wd_stride + c];
     wd[c] = s;
   }
   __syncthreads();
@@ -188,7 +181,7 @@ module_net_kernel(NetParams P) {
   // Weighted degree statistics: two-pass over the k values held in LDS.
   const int64_t woff = off;
   double a1[4] = {0, 0, 0, 0};  // sum(all wd), n, sx, sy
-  for (int64_t c = tid; c < k; c += NR_BS) {
+  for (int64_t c = tid; c < k; c += BS) {
     const double y = wd[c];
     const double xv = P.disc_wd ? P.disc_wd[woff + c] : nr_nan();
     a1[0] += y;
@@ -198,10 +191,10 @@ module_net_kernel(NetParams P) {
       a1[3] += y;
     }
   }
-  block_sums<4>(a1, red);
+  block_sums<4, NW>(a1, red);
   const double mx = a1[2] / a1[1], my = a1[3] / a1[1];
   double a2[3] = {0, 0, 0};
-  for (int64_t c = tid; c < k; c += NR_BS) {
+  for (int64_t c = tid; c < k; c += BS) {
     const double y = wd[c];
     const double xv = P.disc_wd ? P.disc_wd[woff + c] : nr_nan();
     if (isfinite(xv) && isfinite(y)) {
@@ -212,7 +205,7 @@ module_net_kernel(NetParams P) {
     }
     if (P.wd_out) P.wd_out[woff + c] = y;
   }
-  block_sums<3>(a2, red);
+  block_sums<3, NW>(a2, red);
 
   // AverageEdgeWeight src/netStats.cpp:154-162: unsigned int pair count.
   const uint32_t ku = (uint32_t)k;
@@ -228,6 +221,27 @@ module_net_kernel(NetParams P) {
     o[(int64_t)P.n_rows * P.slot_cor_degree] = na_fill(cor_degree);
     o[(int64_t)P.n_rows * P.slot_avg_cor] = na_fill(avg_cor);
   }
+  __syncthreads();  // wd / red free again
+}
+
+// Kernel 1: module network statistics. One workgroup per item.
+__global__ void __launch_bounds__(NR_BS)
+module_net_kernel(NetParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* red = reinterpret_cast<double*>(smem);                    // 8 * NR_WAVES
+  double* wd = red + 8 * NR_WAVES;                                  // [NR_WAVES][k_max]
+  uint32_t* idx = reinterpret_cast<uint32_t*>(wd + NR_WAVES * P.k_max);  // [k]
+  const int64_t item = blockIdx.x;
+  const int64_t mslot = item / P.n_perm;
+  const int64_t p_local = item - mslot * P.n_perm;
+  const int m = P.mod_order[mslot];
+  const int64_t off = P.node_off[m];
+  const int64_t k = P.node_off[m + 1] - off;
+  nr_prp_key key;
+  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
+  for (int64_t c = threadIdx.x; c < k; c += NR_BS) idx[c] = node_index(P.src, key, p_local, off + c);
+  __syncthreads();
+  net_item<NR_WAVES>(P, m, p_local, off, k, idx, red, wd, P.k_max);
 }
 
 // ---------------------------------------------------------------------------
@@ -1221,7 +1235,8 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   int m, k;
   int64_t p_local, off;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
-    NR_STAMP(0);  // queue + index derivation
+    if (P.fuse_net) net_item<NW>(P.net, m, p_local, off, k, L.idx, L.red, part, kmax);
+    NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     // ---- Gram [X 1]^T [X 1] on the matrix cores ----
     double g1[1] = {0.0};
     int bad = 0;
@@ -1615,7 +1630,8 @@ module_profile_reg_kernel(ProfileParams P) {
   int m, k;
   int64_t p_local, off;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
-    NR_STAMP(0);  // queue + index derivation
+    if (P.fuse_net) net_item<NW>(P.net, m, p_local, off, k, L.idx, L.red, rowp, RG_KP);
+    NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     const RgTiles R = rg_tiles(k, wave);
     const int kp = 16 * R.T;
     for (int c = tid; c < kp; c += BS) {
