@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=256, help="permutations per step")
-    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4"])
+    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--cpu-baseline-perms", type=int, default=0,
                     help="CPU sample size (0: sized for ~15 s on the host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -257,7 +257,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic coexpression (SURVEY.md 8d generator), random module layout",
             "config": {"workload": f"{args.config}: {meta['n_nodes']} genes x {meta['n_samples']} samples, "
-                                   f"{len(lay.modules)} modules (30-300 genes), null=overlap, "
+                                   f"{len(lay.modules)} modules ({min(lay.module_sizes)}-{max(lay.module_sizes)} genes), "
+                                   f"null={'all' if args.config == 'C5' else 'overlap'} (pool = every gene), "
                                    f"{'7' if meta['with_data'] else '4'} statistics",
                        "perms_per_step": B, "global_perms": total_perms, "parallelism": f"perm-shard x{world}"},
             "module_perms_per_sec": value * len(lay.modules),

@@ -163,7 +163,10 @@ int fill_na(nr_ctx* ctx, double* d, int64_t n) {
 
 int n_stat_of(const nr_ctx* ctx) { return ctx->d_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA; }
 
-int profile_m_max(int k_max) { return std::min(k_max, 160); }
+// Lanczos basis columns per item: 160 covers every C2/C3 module (<= 46 steps
+// measured); large modules (C5: up to 2,000 nodes, spectra with small gaps)
+// get 320.
+int profile_m_max(int k_max) { return k_max <= 320 ? std::min(k_max, 160) : 320; }
 // Leading dimension of the per-slot Gram: k module columns + the ones column,
 // padded to a 32-column super-tile.
 int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
@@ -177,7 +180,8 @@ int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
 // fallback when the packed layout does not fit LDS):
 // NETREP_PROFILE_VARIANT=reg|packed4|packed|full, NETREP_PROFILE_WG_PER_CU.
 struct ProfilePlan {
-  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave, 3 register-resident
+  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave, 3 register-resident,
+                    // 4 full Gram with the matvec partials in global scratch (large modules)
   int slots = 0;
   int per_cu = 1;
   int64_t gram_doubles = 0, stride = 0;
@@ -194,6 +198,9 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   }
   if (variant == 3 && k_max > nr::reg_kernel_k_max()) variant = 2;
   if (variant != 0 && nr::profile_kernel_lds(k_max, m, n_samples, variant) > 160 * 1024) variant = 0;
+  // Large modules: the per-wave matvec partials (4 x k doubles) move from LDS
+  // to the slot's scratch, which leaves LDS for the six Lanczos vectors only.
+  if (variant == 0 && nr::profile_kernel_lds(k_max, m, n_samples, 0) > 160 * 1024) variant = 4;
   const size_t lds = nr::profile_kernel_lds(k_max, m, n_samples, variant);
   if (lds > 160 * 1024)
     return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
@@ -201,21 +208,21 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   if (const char* e = std::getenv("NETREP_PROFILE_WG_PER_CU")) want = std::max(1, std::min(3, std::atoi(e)));
   if (variant == 1) want = std::min(want, 2);
   if (variant == 2) want = std::max(2, want);
-  if (variant == 3) want = 1;
+  if (variant == 3 || variant == 4) want = 1;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
   plan->variant = variant;
   plan->per_cu = per_cu;
   plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu));
   if (variant == 3) {
     plan->gram_doubles = 0;  // the Gram lives in registers and LDS
-  } else if (variant != 0) {
+  } else if (variant == 1 || variant == 2) {
     const int64_t kc = k_max + 1;
     plan->gram_doubles = (kc * (kc + 1) / 2 + 1 + 31) / 32 * 32;  // packed triangle + zero pad
   } else {
     const int64_t ld = gram_ld(k_max);
     plan->gram_doubles = ld * ld;
   }
-  plan->stride = plan->gram_doubles + (int64_t)k_max * m;
+  plan->stride = plan->gram_doubles + (int64_t)k_max * m + (variant == 4 ? (int64_t)nr::kProfileWaves * k_max : 0);
   return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
 }
 
@@ -296,7 +303,14 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   // kernel (fused per item), so their HBM-bound gathers overlap the matrix and
   // Lanczos work of the co-resident workgroups. NETREP_FUSE=0 launches them
   // as their own kernel (optionally on the side stream, NETREP_CONCURRENT=1).
-  const bool fuse = data && ctx->fuse_net;
+  ProfilePlan plan;
+  if (data) {
+    rc = plan_profile(ctx, n_items, ctx->k_max, (int)ctx->n_samples, &plan);
+    if (rc) return rc;
+  }
+  // Variant 4 keeps its matvec partials in global scratch; the network
+  // statistics (LDS weighted degrees) then run as their own kernel.
+  const bool fuse = data && ctx->fuse_net && plan.variant != 4;
   const bool fork = data && !fuse && ctx->concurrent;
   hipStream_t net_stream = fork ? ctx->side : ctx->stream;
   if (fork) {
@@ -310,9 +324,6 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   }
 
   if (data) {
-    ProfilePlan plan;
-    rc = plan_profile(ctx, n_items, ctx->k_max, (int)ctx->n_samples, &plan);
-    if (rc) return rc;
     NR_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream));
     nr::ProfileParams pp{};
     pp.data = ctx->d_data;
@@ -340,6 +351,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.diag = ctx->d_counters + 1;
     pp.stamps = ctx->d_stamps;
     pp.fuse_net = fuse ? 1 : 0;
+    pp.part_global = plan.variant == 4 ? 1 : 0;
     pp.net = np;
     timer_begin(ctx, 1, ctx->stream);
     NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, ctx->stream));
@@ -782,6 +794,7 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
       pp.scratch_stride = plan.stride;
       pp.queue = ctx->d_counters;
       pp.diag = ctx->d_counters + 1;
+      pp.part_global = plan.variant == 4 ? 1 : 0;
       if (e == hipSuccess) e = nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, ctx->stream);
     }
     auto d2h = [&](double* h, const double* d, int64_t n) {

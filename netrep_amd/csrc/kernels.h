@@ -7,6 +7,8 @@ namespace nr {
 
 enum { NR_IDX_PRP = 0, NR_IDX_TABLE = 1, NR_IDX_DIRECT = 2 };
 
+constexpr int kProfileWaves = 4;  // waves of the 256-thread profile workgroup (NR_WAVES)
+
 // Where the test column of module node c comes from.
 struct IndexSource {
   int mode;                    // NR_IDX_*
@@ -66,6 +68,7 @@ struct ProfileParams {
   int* diag;                   // [0] Lanczos step-cap hits, [1] items, [2] Lanczos steps, [3] reorthogonalisations
   unsigned long long* stamps;  // [8] per-phase shader cycles (diagnostics; NULL = off)
   int fuse_net;                // 1: each item also computes the network statistics (net)
+  int part_global;             // 1: matvec partials (4 x k_max) at the end of the slot's scratch
   NetParams net;
 };
 

@@ -1223,12 +1223,17 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   const int mmax = KB > 0 ? (KB < 160 ? KB : 160) : P.m_max;
   const int S = (int)P.n_samples;
   double* part;
-  const LzLds L = carve_lds<NW>(smem, kmax, mmax, (int64_t)(PACKED ? 2 : 1) * NW * kmax, &part);
-  double* upper = part + NW * kmax;  // packed only
+  // Large modules (variant 4, !PACKED only): the per-wave matvec partials live
+  // in the slot's scratch behind the basis; the workgroup's barriers order
+  // them (one CU, one vector L1).
+  const bool pglob = !PACKED && P.part_global;
+  const LzLds L = carve_lds<NW>(smem, kmax, mmax, pglob ? 0 : (int64_t)(PACKED ? 2 : 1) * NW * kmax, &part);
   const int tid = threadIdx.x;
   double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;  // Gram
   const int ld = P.ld;
   double* Q = G + P.gram_doubles;                                  // Lanczos basis
+  if (pglob) part = Q + (int64_t)kmax * mmax;
+  double* upper = part + NW * kmax;  // packed only
   const double* __restrict__ X = P.data;
   const double Sd = (double)S;
 
@@ -1308,6 +1313,7 @@ constexpr int RG_LT = 4;     // LDS tiles per wave
 constexpr int RG_TMAX = 19;  // tiles a side: k + 1 <= 304
 constexpr int RG_KP = 16 * RG_TMAX;
 constexpr int RG_NTMAX = RG_TMAX * (RG_TMAX + 1) / 2;
+static_assert(kProfileWaves == NR_WAVES, "profile workgroup width");
 static_assert((RG_RT + RG_LT) % 4 == 0, "tile groups of four");
 static_assert(RG_NW * (RG_RT + RG_LT) >= RG_NTMAX, "tile capacity");
 static_assert((RG_NTMAX + RG_NW - 1) / RG_NW <= RG_RT + RG_LT, "per-wave tile capacity");
@@ -1781,6 +1787,8 @@ int reg_kernel_k_max() { return RG_KP - 1; }
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
   (void)n_samples;
   if (variant == 3) return reg_kernel_lds(m_max);
+  if (variant == 4)  // full Gram, matvec partials in global scratch
+    return sizeof(double) * (8 * NR_WAVES + 6 * (size_t)k_max + 12 * (size_t)m_max + 3) + sizeof(uint32_t) * k_max;
   const bool packed = variant != 0;
   const int nw = variant == 1 ? 8 : NR_WAVES;
   if (packed && packed_bucket(k_max) > 0) {

@@ -277,6 +277,38 @@ def test_large_modules_vs_cpp_oracle(seed):
     assert_stats_close(nulls, exp, what="nulls (large modules)")
 
 
+def test_c5_sized_modules_vs_cpp_oracle():
+    """C5-shaped modules (BASELINE configs[4]: up to 2,000 nodes at S = 1,000,
+    so k > S): the large-module layout (full Gram, matvec partials in global
+    scratch, 320-vector Lanczos basis, network statistics as their own
+    kernel) against the C++ restatement (LAPACK dgesdd) on identical shuffles,
+    observed values through IntermediateProperties-shaped discovery vectors."""
+    from netrep_amd import synthetic as S
+    from oracle import ref_cpp
+    seed = 31
+    sizes = [2000, 1100, 600, 250]
+    lay = S.make_layout(7000, sizes, seed)
+    dx, dc, dn = S.numpy_dataset(lay, 1000, seed + 1)
+    tx, tc, tn = S.numpy_dataset(lay, 1000, seed + 2, preserve_all=False)
+    mi = O.ModuleIndex(lay.names, lay.labels, lay.names, lay.modules)
+    disc = O.intermediate_properties(O.scale(dx), dc, dn, mi.disc_idx(lay.names))
+    txs = O.scale(tx)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    seed_p = 77
+    nulls = eng.run(0, 4, seed_p)
+    pis = N.prp_table(seed_p, 0, 4, mi.null_idx.size)
+    mods = mi.mods_present
+    node_off = np.concatenate([[0], np.cumsum([mi.test_idx[m].size for m in mods])])
+    exp, obs = ref_cpp.permutation_procedure(
+        txs, tc, tn, len(mi.modules), [mi.modules.index(m) for m in mods], node_off,
+        np.concatenate([mi.test_idx[m] for m in mods]), np.concatenate([mi.null_pos[m] for m in mods]),
+        mi.null_idx, np.concatenate([disc["corr"][m] for m in mods]),
+        np.concatenate([disc["degree"][m] for m in mods]),
+        np.concatenate([disc["contribution"][m] for m in mods]), 4, pi=pis, n_threads=8)
+    assert_stats_close(eng.observed(), obs, what="observed (C5-sized modules)")
+    assert_stats_close(nulls, exp, what="nulls (C5-sized modules)")
+
+
 def test_netprops_one_node_and_absent_modules(bundled):
     """NetProps keeps AverageEdgeWeight's 0/0 = NaN for a one-node module
     (src/properties.cpp:121, no NaN->NA step for it) and leaves modules with no
