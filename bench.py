@@ -35,6 +35,26 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TFS = 78.6    # MI355X fp64 matrix peak (spec)
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def measured_traffic(config, batch, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
+    (tools/collect_pmc.sh + tools/summarize_pmc.py: FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE, per MI355X_MICROARCH.md). PMC counters cannot be
+    read from inside the timed run, so the number is the one measured on the
+    same command; null when no pass matches this config/batch/kernel."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for r in rows:
+        if r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel:
+            return float(r["hbm_bytes_per_launch"])
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,7 +255,10 @@ def main():
         dom = kernels[dom_name]
         roofline = {"kernel": dom_name, "bound": dom["bound"], "achieved": round(dom["achieved"], 4),
                     "peak": dom["peak"], "unit": dom["unit"], "frac": round(dom["frac"], 6),
-                    "traffic": None}
+                    "traffic": measured_traffic(args.config, B, dom_name),
+                    "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, profiles/pmc_traffic.json)",
+                    "algorithmic_bytes": round(((net_b if fused or dom_name == "module_net_kernel" else 0.0)
+                                                + (prof_b if dom_name == "module_profile_kernel" else 0.0)) * B)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and host is not None:
             rate, dt, n_cpu, threads = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)

@@ -4,6 +4,7 @@ Public surface:
   * ``netrep_amd.api``    -- NetRep's Rcpp entry points (PermutationProcedure, ...)
   * ``netrep_amd.engine`` -- one GPU context over the ``nr_*`` C ABI
   * ``netrep_amd.pvalues``-- the host p-value step (permutationTest)
+  * ``netrep_amd.combine``-- combineAnalyses, the multi-node merge of null cubes
 The compute path is the HIP library ``netrep_amd/_lib/libnetrep_amd.so``.
 """
 from ._lib import NetRepError, load  # noqa: F401
