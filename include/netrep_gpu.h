@@ -64,6 +64,11 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net,
 
 /* 1 if corr and net of the resident dataset are exactly symmetric. */
 int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric);
+/* CheckFinite (src/checkFinite.cpp:21-28) of the resident corr and net,
+ * computed by nr_set_dataset's symmetry pass over the uploaded matrices (no
+ * extra scan): 1 = every element finite. The caller raises the reference's
+ * error ("matrices must not contain NaN/Inf", R/check-user-input.R:796-799). */
+int nr_dataset_finite(nr_ctx* ctx, int* corr_finite, int* net_finite);
 
 /* Module index sets (a4 of SURVEY.md 8) and discovery vectors (a15).
  *   n_rows      rows of the output cube = length of `modules`

@@ -59,6 +59,7 @@ SIGNATURES = {
     "nr_last_error": (C.c_char_p, [_p]),
     "nr_set_dataset": (_int, [_p, _dp, _dp, _dp, _i64, _i64, _int]),
     "nr_dataset_symmetric": (_int, [_p, _intp]),
+    "nr_dataset_finite": (_int, [_p, _intp, _intp]),
     "nr_set_modules": (_int, [_p, _i32, _i32, _i32p, _i64p, _i32p, _i32p, _dp, _dp, _dp]),
     "nr_set_null_pool": (_int, [_p, _i32p, _i64]),
     "nr_observed": (_int, [_p, _dp]),

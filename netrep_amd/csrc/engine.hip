@@ -52,6 +52,7 @@ struct nr_ctx {
   double* d_data = nullptr;
   int64_t n_nodes = 0, n_samples = 0;
   int symmetric = 0;
+  int corr_finite = 0, net_finite = 0;  // CheckFinite of the resident matrices
 
   // modules
   int32_t n_rows = 0, n_present = 0, k_max = 0;
@@ -569,7 +570,9 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
                                ctx->stream));
   }
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  ctx->symmetric = asym ? 0 : 1;
+  ctx->symmetric = (asym & 1) ? 0 : 1;
+  ctx->corr_finite = (asym & 2) ? 0 : 1;
+  ctx->net_finite = (asym & 4) ? 0 : 1;
   return NR_OK;
 }
 
@@ -577,6 +580,14 @@ int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric) {
   if (!ctx || !symmetric) return NR_ERR_INVALID;
   if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset");
   *symmetric = ctx->symmetric;
+  return NR_OK;
+}
+
+int nr_dataset_finite(nr_ctx* ctx, int* corr_finite, int* net_finite) {
+  if (!ctx || !corr_finite || !net_finite) return NR_ERR_INVALID;
+  if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset");
+  *corr_finite = ctx->corr_finite;
+  *net_finite = ctx->net_finite;
   return NR_OK;
 }
 

@@ -1694,27 +1694,34 @@ __global__ void interleave_kernel(const double* __restrict__ corr, const double*
 
 // Exact symmetry check of the interleaved matrix via 32x32 LDS tiles: block
 // (I, J), J >= I, stages A(J, I) in LDS and compares it with A(I, J); both
-// reads are coalesced along rows.
-__global__ void symmetry_kernel(const double2* __restrict__ a, int64_t n, int* asym) {
+// reads are coalesced along rows. The same pass is CheckFinite
+// (src/checkFinite.cpp:21-28) for both matrices of the upload, so the
+// reference's separate full scans (R/check-user-input.R:796-799) cost no extra
+// HBM traffic: every element is read here exactly once (diagonal tiles twice).
+// flags: bit 0 asymmetric, bit 1 corr non-finite, bit 2 net non-finite.
+__global__ void symmetry_kernel(const double2* __restrict__ a, int64_t n, int* flags) {
   __shared__ double2 tile[32][33];
   const int64_t bi = (int64_t)blockIdx.y * 32, bj = (int64_t)blockIdx.x * 32;
   if (bj < bi) return;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  int bad = 0;
   for (int r = ty; r < 32; r += 8) {
     const int64_t row = bj + tx, col = bi + r;               // tile[r][c] = A(bj + c, bi + r)
-    tile[r][tx] = (row < n && col < n) ? a[row + col * n] : make_double2(0.0, 0.0);
+    const double2 v = (row < n && col < n) ? a[row + col * n] : make_double2(0.0, 0.0);
+    bad |= (isfinite(v.x) ? 0 : 2) | (isfinite(v.y) ? 0 : 4);
+    tile[r][tx] = v;
   }
   __syncthreads();
-  int bad = 0;
   for (int r = ty; r < 32; r += 8) {
     const int64_t row = bi + tx, col = bj + r;               // A(bi + c, bj + r) vs tile[c][r]
     if (row < n && col < n) {
       const double2 x = a[row + col * n];
       const double2 t = tile[tx][r];
       bad |= (x.x != t.x) | (x.y != t.y);
+      bad |= (isfinite(x.x) ? 0 : 2) | (isfinite(x.y) ? 0 : 4);
     }
   }
-  if (bad) atomicOr(asym, 1);
+  if (bad) atomicOr(flags, bad);
 }
 
 // Scale (src/scale.cpp:14-25): one wave per column; arma mean + corrected

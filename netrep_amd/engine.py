@@ -95,6 +95,13 @@ class Engine:
         self._check(self._lib.nr_dataset_symmetric(self._h, C.byref(v)))
         return bool(v.value)
 
+    def finite(self):
+        """(corr all finite, net all finite) of the resident dataset -- CheckFinite
+        (src/checkFinite.cpp:21-28) fused into the upload's symmetry pass."""
+        c, n = C.c_int(), C.c_int()
+        self._check(self._lib.nr_dataset_finite(self._h, C.byref(c), C.byref(n)))
+        return bool(c.value), bool(n.value)
+
     # -- modules ----------------------------------------------------------
     def set_modules(self, n_rows, row_of, node_off, test_idx, null_pos, disc_corr, disc_degree,
                     disc_contrib=None):

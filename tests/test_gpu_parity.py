@@ -345,3 +345,27 @@ def test_profile_kernel_variants(variant, monkeypatch, bundled, bundled_expected
     test_bundled_observed_and_nulls_explicit_pi(bundled, bundled_expected, True)
     test_constant_column_gives_na()
     test_engine_synthetic_vs_oracle(True)
+
+
+def test_upload_check_finite_fused():
+    """CheckFinite (src/checkFinite.cpp:21-28) folded into the upload's symmetry
+    pass: per-matrix flags vs numpy's isfinite, on ragged (non-multiple-of-32)
+    sizes and with the bad element in either triangle or on the diagonal."""
+    rng = np.random.default_rng(77)
+    for n, where, what in ((45, (3, 40), "corr"), (45, (40, 3), "net"), (33, (32, 32), "net"),
+                           (70, (0, 69), "corr"), (1, (0, 0), "corr"), (64, None, None)):
+        a = rng.standard_normal((n, n))
+        corr = (a + a.T) / 2
+        net = np.abs(corr) ** 5
+        bad = np.inf if what == "corr" else np.nan
+        if where is not None:
+            (corr if what == "corr" else net)[where] = bad
+        eng = N.Engine(0)
+        try:
+            eng.set_dataset(corr, net)
+            assert eng.finite() == (bool(np.isfinite(corr).all()), bool(np.isfinite(net).all())), (n, where)
+            # exact comparison, so a NaN (even on the diagonal) reads as asymmetric
+            sym = np.array_equal(corr, corr.T) and np.array_equal(net, net.T)
+            assert eng.symmetric() == sym, (n, where)
+        finally:
+            eng.close()
