@@ -138,6 +138,10 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     for (int u = 0; u < U; ++u) {
       const int64_t v = v0 + (int64_t)u * BS;
       jjs[u] = -1;
+      iis[u] = 0;
+      e[u] = make_double2(0.0, 0.0);
+      e2[u] = 0.0;
+      x[u] = 0.0;
       if (v < npairs) {
         int64_t jj, ii;
         decode_pair(v, k, jj, ii);
@@ -151,7 +155,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (jjs[u] < 0) continue;
+      if (jjs[u] >= 0) {
       const double y = e[u].x;
       if (P.cv_out) P.cv_out[cvo + v0 + (int64_t)u * BS] = y;
       atomicAdd(&wdw[jjs[u]], fabs(e[u].y));    // column idx[jj] gains row idx[ii]
@@ -166,6 +170,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
         acc[4] += dy * dy;
         acc[5] += dx * dy;
         acc[6] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
+      }
       }
     }
   }
