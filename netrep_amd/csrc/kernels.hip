@@ -103,7 +103,7 @@ __device__ __forceinline__ void decode_pair(int64_t v, int64_t k, int64_t& jj, i
 // item's test columns; wd is NW x wd_stride doubles of LDS scratch; red holds
 // 8 * NW doubles.
 // ---------------------------------------------------------------------------
-template <int NW>
+template <int NW, int U = 8>
 __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_local, int64_t off, int64_t k,
                                          const uint32_t* idx, double* red, double* wd, int wd_stride) {
   constexpr int BS = NW * 64;
@@ -128,7 +128,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   const double ys = npairs > 0 ? pairs[(int64_t)idx[1] + (int64_t)idx[0] * n].x : 0.0;
 
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // n, sx, sy, sxx, syy, sxy, s(sign(x) y)
-  constexpr int U = 8;  // pairs in flight per thread (random 16-byte gathers)
+  // U: pairs in flight per thread (random 16-byte gathers)
   for (int64_t v0 = tid; v0 < npairs; v0 += (int64_t)BS * U) {
     double2 e[U];
     double e2[U];
@@ -1245,7 +1245,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   int m, k;
   int64_t p_local, off;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
-    if (P.fuse_net) net_item<NW>(P.net, m, p_local, off, k, L.idx, L.red, part, kmax);
+    if (P.fuse_net) net_item<NW, 4>(P.net, m, p_local, off, k, L.idx, L.red, part, kmax);
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     // ---- Gram [X 1]^T [X 1] on the matrix cores ----
     double g1[1] = {0.0};
