@@ -73,3 +73,13 @@ def test_contingency_partial_overlap_and_test_modules():
     assert rows[:2] == ["size", "present"] and cols[:2] == ["size", "present"]
     # every overlapping node is counted once in the body of the table
     assert np.nansum(mat[2:, 2:]) == 6
+
+
+def test_bench_traffic_lookup_matches_committed_pmc():
+    """bench.py reports `roofline.traffic` only from a PMC pass of the same
+    config, batch and kernel (profiles/pmc_traffic.json)."""
+    import bench
+    t = bench.measured_traffic("C3", 256, "module_profile_kernel")
+    assert t is not None and t > 0
+    assert bench.measured_traffic("C3", 512, "module_profile_kernel") is None
+    assert bench.measured_traffic("C2", 256, "module_profile_kernel") is None
