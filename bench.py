@@ -3,14 +3,22 @@
 Workload (BASELINE.json configs[2], the metric's "20k genes x 50 modules"):
 synthetic coexpression, 20,000 genes x 500 samples, 50 modules of
 round(linspace(30, 300, 50)) genes, null = "overlap", all seven statistics.
-A step = one batch of --batch permutations (every module of each) through
-the engine, nulls copied back to host memory. Inputs (test corr, net, scaled
-data, discovery vectors) are resident in HBM before the timed region.
+A step = one nr_run over --perms-per-step permutations (every module of
+each; kernel launches of --launch-batch permutations), nulls copied back to
+host memory. The defaults time 20 x 5,120 = 102,400 permutations per GPU:
+the metric's nPerm = 100k. Inputs (test corr, net, scaled data, discovery
+vectors) are resident in HBM before the timed region.
 
-Multi-GPU: one process per GPU (torchrun). Rank 0 builds the datasets and
-broadcasts the test matrices over RCCL; every rank then evaluates its own
-disjoint permutation range (weak scaling: fixed permutations per GPU), with
-no collective on the data path. Rank 0 prints one JSON line.
+A secondary record times the network-only path on the same 20k-gene
+matrices (BASELINE.json configs[3], C4: the HBM-bound gather kernel) in the
+same run.
+
+Multi-GPU: one process per GPU. `--gpus N` without a torchrun environment
+re-launches this script under torch.distributed.run with N processes before
+any GPU call. Rank 0 builds the datasets and broadcasts the test matrices
+over RCCL; every rank then evaluates its own disjoint permutation range (weak
+scaling: fixed permutations per GPU), with no collective on the data path.
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -60,8 +68,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=256, help="permutations per step")
+    ap.add_argument("--perms-per-step", type=int, default=0,
+                    help="permutations per step (0: 20 launches of --launch-batch)")
+    ap.add_argument("--launch-batch", "--batch", type=int, default=256, dest="batch",
+                    help="permutations per kernel launch")
     ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C4 network-only record")
+    ap.add_argument("--secondary-steps", type=int, default=8)
     ap.add_argument("--cpu-baseline-perms", type=int, default=0,
                     help="CPU sample size (0: sized for ~15 s on the host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -69,6 +82,28 @@ def parse():
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic run: per-phase cycle stamps in the profile kernel")
     return ap.parse_args()
+
+
+def relaunch_if_needed(args):
+    """`--gpus N` (N > 1) outside torchrun: start N ranks under
+    torch.distributed.run as a child process -- before anything touches the
+    GPU -- and exit with its code. Inside torchrun WORLD_SIZE must equal N."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}\n")
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 def setup_dist(args):
@@ -138,15 +173,25 @@ def build_case(cfg, world, rank, local, seed):
     eng.set_modules(len(mods), np.arange(len(mods)), node_off, idx, idx,  # null pool = all genes
                     disc_cv, disc_wd, disc_nc if with_data else None)
     eng.set_null_pool(np.arange(n_nodes, dtype=np.int32))
-    host = None
-    if rank == 0 and world == 1:
-        host = dict(tc=tc, tn=tn, txs=txs)  # kept for the CPU baseline sample
-    else:
-        del tc, tn, txs
-    torch.cuda.empty_cache()
+    # the test tensors stay alive until the secondary (network-only) engine is
+    # built and, on a single rank, for the CPU baseline sample
+    tensors = dict(tc=tc, tn=tn, txs=txs)
     return eng, lay, dict(node_off=node_off, idx=idx, disc_cv=disc_cv, disc_wd=disc_wd,
                           disc_nc=disc_nc, with_data=with_data, n_samples=n_samples,
-                          n_nodes=n_nodes, t_bcast=t_bcast, symmetric=eng.symmetric()), host
+                          n_nodes=n_nodes, t_bcast=t_bcast, symmetric=eng.symmetric()), tensors
+
+
+def secondary_engine(local, meta, tensors):
+    """Network-only engine (C4: permutationsNoData) on the same resident test
+    matrices: the HBM-bound gather kernel as its own driver-timed record."""
+    eng = N.Engine(local)
+    tc, tn = tensors["tc"], tensors["tn"]
+    eng.set_dataset_device(tc.data_ptr(), tn.data_ptr(), 0, meta["n_nodes"], 0)
+    n_mod = meta["node_off"].size - 1
+    eng.set_modules(n_mod, np.arange(n_mod), meta["node_off"], meta["idx"], meta["idx"],
+                    meta["disc_cv"], meta["disc_wd"], None)
+    eng.set_null_pool(np.arange(meta["n_nodes"], dtype=np.int32))
+    return eng
 
 
 def roofline_terms(sizes, n_samples, with_data):
@@ -158,10 +203,41 @@ def roofline_terms(sizes, n_samples, with_data):
     return net_bytes, prof_bytes, prof_flops
 
 
+def time_steps(eng, world, rank, steps, warmup, perms_per_step, seed, base_warm):
+    """W untimed warm-up steps, then K steps bracketed by barrier + device
+    synchronisation; returns (max-over-ranks seconds, local null chunks, base)."""
+    for s_ in range(warmup):
+        p0 = base_warm + s_ * perms_per_step
+        eng.run(p0, p0 + perms_per_step, seed)
+    eng.synchronize()
+    eng.set_timing(True)
+    eng.reset_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    total = world * steps * perms_per_step
+    base, _ = perm_range(rank, world, total)   # this rank's contiguous chunk
+    chunks = []
+    for s_ in range(steps):
+        p0 = base + s_ * perms_per_step
+        chunks.append(eng.run(p0, p0 + perms_per_step, seed))
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, chunks, total
+
+
 def cpu_baseline(lay, meta, host, n_perm, seed):
     """The C++ CPU restatement of the reference's path (oracle/netrep_ref.cpp:
     per-thread contiguous permutation chunks, one null-pool shuffle per
-    permutation, LAPACK dgesdd per module) on a bounded sample of the same
+    permutation, LAPACK dgesvd per module) on a bounded sample of the same
     workload, using the host cores of this GPU's share (at most 16)."""
     from oracle import ref_cpp
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -187,50 +263,64 @@ def cpu_baseline(lay, meta, host, n_perm, seed):
 
 def main():
     args = parse()
+    relaunch_if_needed(args)
     world, rank, local = setup_dist(args)
-    eng, lay, meta, host = build_case(args.config, world, rank, local, args.seed)
+    eng, lay, meta, tensors = build_case(args.config, world, rank, local, args.seed)
     B, K, W = args.batch, args.steps, args.warmup
+    P = args.perms_per_step or 20 * B
     eng.set_batch(B)
     net_b, prof_b, prof_f = roofline_terms(lay.module_sizes, meta["n_samples"], meta["with_data"])
+    n_cfg, s_cfg, sizes_cfg, _, _ = S.CONFIGS[args.config]
 
-    def step(s, base):
-        p0 = base + s * B
-        return eng.run(p0, p0 + B, args.seed)
+    eng2 = None
+    if not args.no_secondary and meta["with_data"] and args.config == "C3":
+        eng2 = secondary_engine(local, meta, tensors)
+    host = tensors if (rank == 0 and world == 1) else None
+    if host is None:
+        del tensors
+    torch.cuda.empty_cache()
 
-    base_w = 10**12 + rank * W * B        # warm-up permutations, outside the measured range
-    for s in range(W):
-        step(s, base_w)
-    eng.synchronize()
-    eng.set_timing(True)
-    eng.reset_timing()
     if args.stamps:
         eng.set_stamps(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    total_perms = world * K * B
-    base, _ = perm_range(rank, world, total_perms)   # this rank's contiguous chunk
-    chunks = []
-    for s in range(K):
-        chunks.append(step(s, base))
-    eng.synchronize()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, chunks, total_perms = time_steps(eng, world, rank, K, W, P, args.seed, 10**12 + rank * W * P)
     ms0, l0, _ = eng.timing(0)
     ms1, l1, _ = eng.timing(1)
-    local = np.concatenate(chunks, axis=2)
-    cube = gather_nulls(local, rank, world, total_perms) if world > 1 else local
-    finite = float(np.isfinite(cube).mean()) if rank == 0 else None
     diag = eng.diagnostics()
     if args.stamps:
         diag["stamps_cycles"] = eng.stamps()
+    local_cube = np.concatenate(chunks, axis=2)
+    del chunks
+    cube = gather_nulls(local_cube, rank, world, total_perms) if world > 1 else local_cube
+    finite = float(np.isfinite(cube).mean()) if rank == 0 else None
+    del cube, local_cube
+
+    # -- secondary record: network-only (C4) on the same matrices ---------------
+    secondary = None
+    if eng2 is not None:
+        B2 = 1024
+        P2 = 16 * B2
+        eng2.set_batch(B2)
+        el2, ch2, tot2 = time_steps(eng2, world, rank, args.secondary_steps, 1, P2, args.seed + 1,
+                                    2 * 10**12 + rank * P2)
+        ms2, l2, _ = eng2.timing(0)
+        fin2 = float(np.isfinite(np.concatenate(ch2, axis=2)).mean())
+        del ch2
+        if rank == 0:
+            t2 = ms2 / max(l2, 1) / 1e3
+            secondary = {
+                "metric": "permutations/sec (whole node), network-only path (permutationsNoData), "
+                          f"{n_cfg // 1000}k nodes x {len(lay.modules)} modules",
+                "config": "C4 (BASELINE.json configs[3]) on the same resident 20k-gene matrices",
+                "value": tot2 / el2, "unit": "permutations/sec", "steps": args.secondary_steps,
+                "perms_per_step": P2, "launch_batch": B2, "ms_per_step": el2 / args.secondary_steps * 1e3,
+                "finite_fraction": fin2,
+                "roofline": {"kernel": "module_net_kernel", "bound": "hbm", "avg_ms": ms2 / max(l2, 1),
+                             "achieved": net_b * B2 / t2 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": net_b * B2 / t2 / 1e9 / HBM_PEAK_GBS,
+                             "traffic": measured_traffic("C4", B2, "module_net_kernel"),
+                             "algorithmic_bytes": round(net_b * B2)},
+            }
+        eng2.close()
 
     if rank == 0:
         value = total_perms / elapsed
@@ -265,9 +355,11 @@ def main():
             cpu = {"value": rate, "unit": "permutations/sec", "cores": threads, "kind": "port",
                    "sample": f"{n_cpu} permutations x {len(lay.modules)} modules of the same workload in "
                              f"{dt:.1f} s: C++ restatement of src/permutations.cpp (std::thread chunks, "
-                             f"LAPACK dgesdd), {threads} threads"}
+                             f"LAPACK SVD), {threads} threads"}
+        null_desc = "all" if args.config == "C5" else "overlap"
         line = {
-            "metric": "permutations/sec (whole node), 20k genes x 50 modules",
+            "metric": f"permutations/sec (whole node), {n_cfg // 1000}k genes x {len(sizes_cfg)} modules"
+                      + ("" if meta["with_data"] else " (network only)"),
             "value": value,
             "unit": "permutations/sec",
             "n_gpus": world,
@@ -281,14 +373,16 @@ def main():
             "data": "synthetic coexpression (SURVEY.md 8d generator), random module layout",
             "config": {"workload": f"{args.config}: {meta['n_nodes']} genes x {meta['n_samples']} samples, "
                                    f"{len(lay.modules)} modules ({min(lay.module_sizes)}-{max(lay.module_sizes)} genes), "
-                                   f"null={'all' if args.config == 'C5' else 'overlap'} (pool = every gene), "
+                                   f"null={null_desc} (pool = every gene), "
                                    f"{'7' if meta['with_data'] else '4'} statistics",
-                       "perms_per_step": B, "global_perms": total_perms, "parallelism": f"perm-shard x{world}"},
+                       "perms_per_step": P, "launch_batch": B, "global_perms": total_perms,
+                       "parallelism": f"perm-shard x{world}"},
             "module_perms_per_sec": value * len(lay.modules),
             "algorithmic_GBps": value * (net_b + prof_b) / 1e9,
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,
+            "secondary": secondary,
             "finite_fraction": finite,
             "broadcast_s": meta["t_bcast"],
             "symmetric_matrices": meta["symmetric"],

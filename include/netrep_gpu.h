@@ -62,6 +62,11 @@ const char* nr_last_error(const nr_ctx* ctx);
 int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net,
                    const double* data, int64_t n_nodes, int64_t n_samples, int where);
 
+/* Make src's resident dataset resident in dst too, device to device (over
+ * xGMI when the contexts are on different GPUs): the host matrices cross PCIe
+ * once, to the first GPU, and fan out from there. */
+int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src);
+
 /* 1 if corr and net of the resident dataset are exactly symmetric. */
 int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric);
 /* CheckFinite (src/checkFinite.cpp:21-28) of the resident corr and net,
@@ -104,7 +109,16 @@ int nr_observed(nr_ctx* ctx, double* observed);
  * pi == NULL: permutation p draws pi_p = keyed PRP(seed, p) (prp.h).
  * pi != NULL: explicit host table [(perm_end-perm_begin) x n_null] of
  *   null-pool permutations, pi[p][q] = source position (the exported
- *   shuffles of the reference, src/permutations.cpp:63).
+ *   shuffles of the reference, src/permutations.cpp:63). The table must hold
+ *   exactly that many entries, each < n_null; an entry >= n_null is rejected
+ *   with NR_ERR_INVALID before anything runs (device tables are checked by a
+ *   device scan). Module nodes' null_pos (nr_set_modules) must be < n_null
+ *   (NR_ERR_INVALID otherwise).
+ * Cancellation: nr_cancel (any thread) stops the run in progress -- or the
+ *   next one started on ctx -- between launches; it returns NR_ERR_CANCELLED
+ *   with every slice not computed set to NA_real_ (the reference's
+ *   interrupted workers leave their part of the NA-filled cube,
+ *   src/permutations.cpp:375-384).
  * nulls receives (perm_end-perm_begin) slices of n_rows x n_stat, i.e. the
  * cube layout m + n_rows*s + n_rows*n_stat*p of src/permutations.cpp:55
  * starting at permutation perm_begin. Host pointer for nr_run, device pointer
@@ -185,12 +199,29 @@ typedef struct netrep_disc_props {
   const int64_t* contribution_len;
 } netrep_disc_props;
 
+/* Interrupt hook: the replacement of checkInterrupt (src/interrupt.cpp:9-11)
+ * as polled by MonitorProgress (src/thread-utils.cpp:49-82). While
+ * netrep_PermutationProcedure runs, its calling thread polls fn(user) every
+ * 100 ms (the engine works on other host threads); a non-zero return cancels
+ * every GPU's run. The R glue installs a function that wraps
+ * R_ToplevelExec(R_CheckUserInterrupt). NULL removes it.
+ * Process-wide; set it before the call. */
+typedef int (*netrep_interrupt_fn)(void* user);
+void netrep_set_interrupt_hook(netrep_interrupt_fn fn, void* user);
+
 /* PermutationProcedure (src/permutations.cpp:160-166) and
  * PermutationProcedureNoData (src/permutationsNoData.cpp:140-146, t_data =
  * NULL). nulls_out [n_modules x n_stat x n_perm], observed_out
  * [n_modules x n_stat], both column-major, NA-filled. `seed` keys the PRP;
  * `pi` (optional, [n_perm x n_null]) supplies explicit shuffles. n_cores is
- * accepted for interface parity; NETREP_NUM_GPUS selects the GPU count. */
+ * accepted for interface parity; NETREP_NUM_GPUS selects the GPU count
+ * (NETREP_SHARE_DEVICE=1 lets several contexts share the visible GPUs, a test
+ * mode for the sharded path on a one-GPU machine). The test matrices are
+ * uploaded once, to the first GPU, and copied device to device to the others.
+ * Interrupted (netrep_set_interrupt_hook): returns NR_ERR_CANCELLED with
+ * observed_out complete and nulls_out holding every completed permutation,
+ * NA_real_ elsewhere -- the partial cube the reference returns
+ * (src/permutations.cpp:375-408). */
 int netrep_PermutationProcedure(
     const netrep_disc_props* disc_props, const double* t_data,
     const double* t_corr, const double* t_net, int64_t n_samples,

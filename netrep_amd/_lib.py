@@ -42,6 +42,7 @@ _i64p = C.POINTER(C.c_int64)
 _u32p = C.POINTER(C.c_uint32)
 _intp = C.POINTER(C.c_int)
 _strv = C.POINTER(C.c_char_p)
+INTERRUPT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p)   # netrep_interrupt_fn
 
 
 class DiscProps(C.Structure):
@@ -58,6 +59,7 @@ SIGNATURES = {
     "nr_ctx_destroy": (None, [_p]),
     "nr_last_error": (C.c_char_p, [_p]),
     "nr_set_dataset": (_int, [_p, _dp, _dp, _dp, _i64, _i64, _int]),
+    "nr_copy_dataset": (_int, [_p, _p]),
     "nr_dataset_symmetric": (_int, [_p, _intp]),
     "nr_dataset_finite": (_int, [_p, _intp, _intp]),
     "nr_set_modules": (_int, [_p, _i32, _i32, _i32p, _i64p, _i32p, _i32p, _dp, _dp, _dp]),
@@ -91,6 +93,7 @@ SIGNATURES = {
     "netrep_Scale": (_int, [_dp, _i64, _i64, _dp]),
     "netrep_CheckFinite": (_int, [_dp, _i64, _i64]),
     "netrep_last_error": (C.c_char_p, []),
+    "netrep_set_interrupt_hook": (None, [C.c_void_p, C.c_void_p]),
 }
 
 _lib = None

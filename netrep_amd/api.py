@@ -144,6 +144,36 @@ def IntermediatePropertiesNoData(dCorr: RMatrix, dNet: RMatrix, tNodeNames, modu
     return _intermediate(None, dCorr, dNet, list(tNodeNames), moduleAssignments, modules)
 
 
+def _null_pool_size(ma_names, t_names, null_hypothesis) -> int:
+    """|nullIdx| of MakeNullMap (src/utils.cpp:108-136) over validNodes
+    (src/permutations.cpp:319-323)."""
+    tset = set(t_names)
+    if str(null_hypothesis) == "all":
+        return len(tset)
+    return len({nm for nm in ma_names if nm in tset})
+
+
+_hook_keep = None
+
+
+def set_interrupt_hook(fn) -> None:
+    """Install ``fn() -> bool`` as the interrupt check polled (every 100 ms) by
+    PermutationProcedure while the GPUs work (checkInterrupt,
+    src/interrupt.cpp:9-11, in MonitorProgress, src/thread-utils.cpp:49-82).
+    A true return cancels the run; the call then returns the partial cube
+    (un-run permutations NA) with ``res["interrupted"] = True``. ``None``
+    removes the hook."""
+    global _hook_keep
+    lib = L.load()
+    if fn is None:
+        lib.netrep_set_interrupt_hook(None, None)
+        _hook_keep = None
+        return
+    cb = L.INTERRUPT_FN(lambda _user: 1 if fn() else 0)
+    _hook_keep = cb
+    lib.netrep_set_interrupt_hook(C.cast(cb, C.c_void_p), None)
+
+
 def _permutation(disc_props, t_data, t_corr, t_net, module_assignments, modules, n_perm, n_cores,
                  null_hypothesis, verbose, seed, pi):
     lib = L.load()
@@ -182,17 +212,27 @@ def _permutation(disc_props, t_data, t_corr, t_net, module_assignments, modules,
     pi_arr = None
     if pi is not None:
         pi_arr = np.ascontiguousarray(pi, dtype=np.uint32)
+        n_null = _null_pool_size(names, t_names, null_hypothesis)
+        if pi_arr.ndim != 2 or pi_arr.shape != (int(n_perm), n_null):
+            raise L.NetRepError(L.NR_ERR_INVALID, f"pi must have shape (nPermutations, n_null) = "
+                                                  f"({int(n_perm)}, {n_null}), got {pi_arr.shape}")
     tn, _k1 = _strv(t_names)
     an, _k2 = _strv(names)
     al, _k3 = _strv(labels)
     mo, _k4 = _strv(modules)
-    L.check_api(lib.netrep_PermutationProcedure(
+    rc = lib.netrep_PermutationProcedure(
         C.byref(dp), _dptr(data), _dptr(corr), _dptr(net), s, n, tn, an, al, len(names), mo, nm_,
         int(n_perm), int(n_cores), str(null_hypothesis).encode(), int(bool(verbose)),
         int(seed) & (2**64 - 1), pi_arr.ctypes.data_as(C.POINTER(C.c_uint32)) if pi_arr is not None else None,
-        _dptr(nulls), _dptr(observed)))
+        _dptr(nulls), _dptr(observed))
+    interrupted = rc == L.NR_ERR_CANCELLED
+    if not interrupted:
+        L.check_api(rc)
     statnames = STATNAMES if with_data else STATNAMES_NODATA
     res = {"observed": observed, "observed_dimnames": (modules, statnames)}
+    if interrupted:
+        # the reference returns the partial, NA-padded cube (src/permutations.cpp:375-408)
+        res["interrupted"] = True
     if n_perm > 0:
         res["nulls"] = nulls
         res["nulls_dimnames"] = (modules, statnames, None)  # "permutation.i" left implicit

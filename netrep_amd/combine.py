@@ -63,7 +63,8 @@ def combine_analyses_internal(pres1: dict, pres2: dict) -> dict:
     res["nulls"] = np.concatenate([np.asarray(pres1["nulls"]), np.asarray(pres2["nulls"])], axis=2)
     res["p.values"] = permutationTest(res["nulls"], res["observed"], res["nVarsPresent"],
                                       res["totalSize"], res["alternative"],
-                                      statnames=pres1.get("statnames"))
+                                      statnames=pres1.get("statnames"),
+                                      modules=pres1.get("modules", pres1.get("observed_dimnames", [None])[0]))
     return res
 
 

@@ -13,14 +13,28 @@ from collections import Counter, OrderedDict
 import numpy as np
 
 
-def order_as_numeric(labels):
-    """R/utils.R:175-181."""
-    labels = [str(x) for x in labels]
+def _r_as_integer(x: str):
+    """R's as.integer() on one character value: decimal / scientific notation
+    truncated toward zero ("1.0" -> 1, "1e3" -> 1000, " 7 " -> 7); None where R
+    gives NA with a warning (not a number, or outside the int32 range)."""
     try:
-        keys = [int(x) for x in labels]
-        return [labels[i] for i in sorted(range(len(labels)), key=lambda i: keys[i])]
+        v = float(x.strip())
     except ValueError:
+        return None
+    if not np.isfinite(v) or abs(v) >= 2**31:
+        return None
+    return int(v)
+
+
+def order_as_numeric(labels):
+    """orderAsNumeric (R/utils.R:175-181): order by as.integer(labels) (stable,
+    as R's order), or -- when as.integer warns for any label -- by the labels
+    as characters. R collates characters by locale; this uses code points."""
+    labels = [str(x) for x in labels]
+    keys = [_r_as_integer(x) for x in labels]
+    if any(k is None for k in keys):
         return sorted(labels)
+    return [labels[i] for i in sorted(range(len(labels)), key=lambda i: keys[i])]
 
 
 def _table(values):
@@ -48,7 +62,9 @@ def contingencyTable(modAssignments, mods, tiNodelist):
     order = order_as_numeric(list(vp))
     vars_pres = OrderedDict((m, vp[m]) for m in order)
     sizes = _table(disc.values())
-    prop = OrderedDict((m, vars_pres[m] / sizes[m]) for m in vars_pres if m in sizes)
+    # varsPres / moduleSizes[names(varsPres)]: NA for a module with no node in
+    # the discovery assignments (R/contingency.R:52-53)
+    prop = OrderedDict((m, vars_pres[m] / sizes[m] if m in sizes else np.nan) for m in vars_pres)
     contingency = None
     if test is not None:
         d_lab = sorted(set(disc[n] for n in overlap_vars))
@@ -59,6 +75,10 @@ def contingencyTable(modAssignments, mods, tiNodelist):
         test_present = _table(test[n] for n in overlap_vars if n in test)
         rows = d_lab + [m for m in disc_sizes if m not in d_lab]
         cols = t_lab + [m for m in test_sizes if m not in t_lab]
+        missing = [m for m in mods if m not in rows]
+        if missing:   # contingency[mods,, drop=FALSE] (R/contingency.R:95)
+            raise ValueError("subscript out of bounds: module(s) " + ", ".join(f'"{m}"' for m in missing)
+                             + " have no node in the discovery module assignments")
         rows = order_as_numeric([r for r in mods if r in rows or r in disc_sizes])
         cols = order_as_numeric(cols)
         mat = np.full((2 + len(rows), 2 + len(cols)), np.nan)

@@ -57,6 +57,7 @@ struct nr_ctx {
   // modules
   int32_t n_rows = 0, n_present = 0, k_max = 0;
   int64_t n_node_total = 0, n_cv_total = 0;
+  int64_t null_pos_max = -1;  // largest null-pool position of any module node (-1: none)
   std::vector<int64_t> node_off_h, cv_off_h;
   int32_t* d_row_of = nullptr;
   int64_t* d_node_off = nullptr;
@@ -379,7 +380,44 @@ int check_ready(nr_ctx* ctx, bool need_null) {
   if (ctx->n_rows <= 0) return fail(ctx, NR_ERR_INVALID, "no modules: call nr_set_modules first");
   if (need_null && ctx->n_present > 0 && (!ctx->d_null_idx || !ctx->d_null_pos))
     return fail(ctx, NR_ERR_INVALID, "no null pool: call nr_set_null_pool and pass null_pos");
+  // Every permuted index is null_idx[pi(null_pos)]: a position outside the pool
+  // would be read out of bounds on the device.
+  if (need_null && ctx->n_present > 0 && ctx->null_pos_max >= ctx->n_null)
+    return fail(ctx, NR_ERR_INVALID, "null_pos outside the null pool (a module node position >= n_null)");
   return NR_OK;
+}
+
+// An explicit shuffle table must hold n_perm x n_null entries, each < n_null
+// (pi[p][q] is a null-pool position). Checked before anything is launched.
+int check_pi_host(nr_ctx* ctx, const uint32_t* pi, int64_t n_perm) {
+  const uint64_t n = (uint64_t)n_perm * (uint64_t)ctx->n_null;
+  const uint32_t lim = (uint32_t)ctx->n_null;
+  uint32_t bad = 0;
+  for (uint64_t i = 0; i < n; ++i) bad |= (uint32_t)(pi[i] >= lim);
+  return bad ? fail(ctx, NR_ERR_INVALID, "pi holds an entry >= n_null (explicit shuffles are null-pool positions)")
+             : NR_OK;
+}
+
+__global__ void pi_check_kernel(const uint32_t* __restrict__ pi, int64_t n, uint32_t lim, int* flag) {
+  int bad = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= pi[i] >= lim;
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+int check_pi_device(nr_ctx* ctx, const uint32_t* d_pi, int64_t n_perm) {
+  const int64_t n = n_perm * ctx->n_null;
+  if (n == 0) return NR_OK;
+  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 6, 0, sizeof(int), ctx->stream));
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(pi_check_kernel, dim3(g), dim3(256), 0, ctx->stream, d_pi, n, (uint32_t)ctx->n_null,
+                     ctx->d_counters + 6);
+  NR_HIP(ctx, hipGetLastError());
+  int bad = 0;
+  NR_HIP(ctx, hipMemcpyAsync(&bad, ctx->d_counters + 6, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return bad ? fail(ctx, NR_ERR_INVALID, "pi holds an entry >= n_null (explicit shuffles are null-pool positions)")
+             : NR_OK;
 }
 
 int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* pi, bool pi_on_device,
@@ -392,10 +430,29 @@ int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* p
   const int64_t batch = auto_batch(ctx);
   ctx->done = 0;
   ctx->total = e - b;
-  ctx->cancel = false;
   NR_HIP(ctx, hipSetDevice(ctx->device));
+  if (pi && e > b) {
+    rc = pi_on_device ? check_pi_device(ctx, pi, e - b) : check_pi_host(ctx, pi, e - b);
+    if (rc) return rc;
+  }
+  // A cancellation (nr_cancel, from any thread, before or during the run) is
+  // honoured between launches: the slices not yet computed are left NA, as
+  // the reference's interrupted workers leave their part of the NA-filled cube
+  // (src/permutations.cpp:375-384), and the flag is consumed.
+  auto cancelled = [&](int64_t p_stop) -> int {
+    ctx->cancel = false;
+    const double na = [] { uint64_t u = 0x7FF00000000007A2ull; double d; std::memcpy(&d, &u, 8); return d; }();
+    if (nulls_on_device) {
+      int r2 = fill_na(ctx, nulls + (p_stop - b) * slice, (e - p_stop) * slice);
+      if (r2) return r2;
+      NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    } else {
+      std::fill(nulls + (p_stop - b) * slice, nulls + (e - b) * slice, na);
+    }
+    return fail(ctx, NR_ERR_CANCELLED, "permutation procedure cancelled");
+  };
   for (int64_t p0 = b; p0 < e; p0 += batch) {
-    if (ctx->cancel.load()) return fail(ctx, NR_ERR_CANCELLED, "permutation procedure cancelled");
+    if (ctx->cancel.load()) return cancelled(p0);
     const int64_t np = std::min(batch, e - p0);
     const uint32_t* d_pi = nullptr;
     if (pi) {
@@ -434,6 +491,7 @@ int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* p
     }
     ctx->done += np;
   }
+  ctx->cancel = false;  // a cancellation that arrives after the last launch has nothing left to stop
   return NR_OK;
 }
 
@@ -576,6 +634,31 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   return NR_OK;
 }
 
+int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
+  if (!dst || !src || dst == src) return NR_ERR_INVALID;
+  if (!src->d_pairs) return fail(dst, NR_ERR_INVALID, "source context has no dataset");
+  NR_HIP(dst, hipSetDevice(dst->device));
+  NR_HIP(dst, hipStreamSynchronize(dst->stream));
+  dfree(dst->d_pairs);
+  dfree(dst->d_data);
+  const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2);
+  NR_HIP(dst, hipMalloc((void**)&dst->d_pairs, pair_bytes));
+  if (src->d_data) NR_HIP(dst, hipMalloc((void**)&dst->d_data, (size_t)(src->n_samples * src->n_nodes) * sizeof(double)));
+  // Device to device: over xGMI between GPUs, an on-device copy when both
+  // contexts share a GPU. The source must be idle (its upload synchronised).
+  NR_HIP(dst, hipMemcpyPeerAsync(dst->d_pairs, dst->device, src->d_pairs, src->device, pair_bytes, dst->stream));
+  if (src->d_data)
+    NR_HIP(dst, hipMemcpyPeerAsync(dst->d_data, dst->device, src->d_data, src->device,
+                                   (size_t)(src->n_samples * src->n_nodes) * sizeof(double), dst->stream));
+  NR_HIP(dst, hipStreamSynchronize(dst->stream));
+  dst->n_nodes = src->n_nodes;
+  dst->n_samples = src->n_samples;
+  dst->symmetric = src->symmetric;
+  dst->corr_finite = src->corr_finite;
+  dst->net_finite = src->net_finite;
+  return NR_OK;
+}
+
 int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric) {
   if (!ctx || !symmetric) return NR_ERR_INVALID;
   if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset");
@@ -630,6 +713,13 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   for (int64_t i = 0; i < ctx->n_node_total; ++i)
     if (test_idx[i] < 0 || test_idx[i] >= ctx->n_nodes)
       return fail(ctx, NR_ERR_INVALID, "test_idx outside the resident dataset (call nr_set_dataset first)");
+  ctx->null_pos_max = -1;
+  if (null_pos) {
+    for (int64_t i = 0; i < ctx->n_node_total; ++i) {
+      if (null_pos[i] < 0) return fail(ctx, NR_ERR_INVALID, "negative null_pos");
+      ctx->null_pos_max = std::max<int64_t>(ctx->null_pos_max, null_pos[i]);
+    }
+  }
   std::vector<int32_t> order(n_present);
   for (int m = 0; m < n_present; ++m) order[m] = m;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {

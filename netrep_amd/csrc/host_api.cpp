@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -83,12 +84,34 @@ int open_ctx(int device, CtxPtr& out) {
   return NR_OK;
 }
 
-int gpu_count_requested() {
+// Contexts requested by NETREP_NUM_GPUS, clamped to the visible GPUs unless
+// NETREP_SHARE_DEVICE=1 (test mode: contexts share GPUs round-robin, so the
+// sharded chunk/merge path runs on a one-GPU machine).
+int gpu_count_requested(int* avail_out) {
   int avail = 0;
   nr_device_count(&avail);
+  *avail_out = std::max(avail, 1);
   int want = 1;
   if (const char* e = std::getenv("NETREP_NUM_GPUS")) want = std::max(1, std::atoi(e));
+  const char* share = std::getenv("NETREP_SHARE_DEVICE");
+  if (share && std::atoi(share) != 0) return std::min(want, 64);
   return std::max(1, std::min(want, avail));
+}
+
+// checkInterrupt replacement (netrep_set_interrupt_hook).
+std::mutex g_hook_mu;
+netrep_interrupt_fn g_hook = nullptr;
+void* g_hook_user = nullptr;
+
+bool interrupt_requested() {
+  netrep_interrupt_fn fn;
+  void* user;
+  {
+    std::lock_guard<std::mutex> lk(g_hook_mu);
+    fn = g_hook;
+    user = g_hook_user;
+  }
+  return fn != nullptr && fn(user) != 0;
 }
 
 // Index sets of the modules present in the test dataset (a4 of SURVEY.md 8).
@@ -106,6 +129,12 @@ struct ModuleSets {
 extern "C" {
 
 const char* netrep_last_error(void) { return g_err.c_str(); }
+
+void netrep_set_interrupt_hook(netrep_interrupt_fn fn, void* user) {
+  std::lock_guard<std::mutex> lk(g_hook_mu);
+  g_hook = fn;
+  g_hook_user = user;
+}
 
 int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_data,
                                 const double* t_corr, const double* t_net, int64_t n_samples,
@@ -170,18 +199,20 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
   ms.n_present = (int32_t)ms.row_of.size();
   const int n_stat = with_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA;
 
-  const int n_gpu = (n_perm > 0) ? (int)std::min<int64_t>(gpu_count_requested(), std::max<int64_t>(n_perm, 1)) : 1;
+  int n_dev = 1;
+  const int n_gpu = (n_perm > 0) ? (int)std::min<int64_t>(gpu_count_requested(&n_dev), std::max<int64_t>(n_perm, 1)) : 1;
   std::vector<CtxPtr> ctxs(n_gpu);
   for (int g = 0; g < n_gpu; ++g) {
-    int rc = open_ctx(g, ctxs[g]);
+    int rc = open_ctx(g % n_dev, ctxs[g]);
     if (rc) return rc;
   }
-  // Each GPU holds its own copy of the test dataset (the multi-rank driver in
-  // bench.py broadcasts it over RCCL instead).
+  // The host matrices cross PCIe once, into the first GPU; the other GPUs
+  // receive them device to device over xGMI (nr_copy_dataset), concurrently.
   std::vector<int> rcs(n_gpu, NR_OK);
   auto setup = [&](int g) {
     nr_ctx* c = ctxs[g].get();
-    int rc = nr_set_dataset(c, t_corr, t_net, t_data, n_nodes, n_samples, NR_HOST);
+    int rc = g == 0 ? nr_set_dataset(c, t_corr, t_net, t_data, n_nodes, n_samples, NR_HOST)
+                    : nr_copy_dataset(c, ctxs[0].get());
     if (!rc)
       rc = nr_set_modules(c, ms.n_rows, ms.n_present, ms.row_of.data(), ms.node_off.data(),
                           ms.test_idx.data(), ms.null_pos.data(), ms.disc_cv.data(),
@@ -189,9 +220,11 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
     if (!rc && !ms.null_idx.empty()) rc = nr_set_null_pool(c, ms.null_idx.data(), (int64_t)ms.null_idx.size());
     rcs[g] = rc;
   };
+  setup(0);
+  if (rcs[0]) return ctx_err(rcs[0], ctxs[0].get());
   {
     std::vector<std::thread> th;
-    for (int g = 0; g < n_gpu; ++g) th.emplace_back(setup, g);
+    for (int g = 1; g < n_gpu; ++g) th.emplace_back(setup, g);
     for (auto& t : th) t.join();
   }
   for (int g = 0; g < n_gpu; ++g)
@@ -215,16 +248,26 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
     std::printf("\n");
     std::fflush(stdout);
   }
+  std::atomic<int> running{n_gpu};
   std::vector<std::thread> th;
   for (int g = 0; g < n_gpu; ++g) {
     th.emplace_back([&, g]() {
       rcs[g] = nr_run(ctxs[g].get(), start[g], start[g + 1], seed,
                       pi ? pi + start[g] * n_null : nullptr, nulls_out + start[g] * slice);
+      running.fetch_sub(1);
     });
   }
-  // Progress monitor (MonitorProgress, src/thread-utils.cpp:49-82).
-  if (verbose) {
-    for (;;) {
+  // Progress monitor (MonitorProgress, src/thread-utils.cpp:49-82): the
+  // calling thread polls progress and the interrupt hook every 100 ms and
+  // prints "% completed." once a second when verbose. On an interrupt every
+  // context is cancelled; the workers stop between launches and leave their
+  // remaining slices NA, and the partial cube is returned
+  // (src/permutations.cpp:375-408) with NR_ERR_CANCELLED.
+  bool interrupted = false;
+  auto last_print = std::chrono::steady_clock::now() - std::chrono::seconds(1);
+  for (;;) {
+    const bool done_all = running.load() == 0;
+    if (verbose && (done_all || std::chrono::steady_clock::now() - last_print >= std::chrono::seconds(1))) {
       int64_t done = 0;
       for (int g = 0; g < n_gpu; ++g) {
         int64_t d = 0;
@@ -234,18 +277,29 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
       const unsigned pct = (unsigned)std::lround((double)done / (double)n_perm * 100.0);
       std::printf("\r%5u%% completed.", pct);
       std::fflush(stdout);
-      if (done >= n_perm) break;
-      bool any_failed = false;
-      for (int g = 0; g < n_gpu; ++g) any_failed |= rcs[g] != NR_OK;
-      if (any_failed) break;
-      std::this_thread::sleep_for(std::chrono::milliseconds(200));
+      last_print = std::chrono::steady_clock::now();
     }
+    if (done_all) break;
+    if (!interrupted && interrupt_requested()) {
+      interrupted = true;
+      for (int g = 0; g < n_gpu; ++g) nr_cancel(ctxs[g].get());
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  }
+  if (verbose) {
     std::printf("\n\n");
     std::fflush(stdout);
   }
   for (auto& t : th) t.join();
-  for (int g = 0; g < n_gpu; ++g)
+  int cancelled_at = -1;
+  for (int g = 0; g < n_gpu; ++g) {
+    if (rcs[g] == NR_ERR_CANCELLED) {
+      if (cancelled_at < 0) cancelled_at = g;
+      continue;
+    }
     if (rcs[g]) return ctx_err(rcs[g], ctxs[g].get());
+  }
+  if (cancelled_at >= 0) return ctx_err(NR_ERR_CANCELLED, ctxs[cancelled_at].get());
   return NR_OK;
 }
 

@@ -124,8 +124,12 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   const int64_t n = P.n_nodes;
   // Shifts keep the one-pass sums well conditioned and make a constant
   // vector give exactly zero variance, as the reference's two-pass stddev does.
+  // The test-side shift is the item's first pair; a non-finite first pair
+  // (dropped by CompleteCases, src/netStats.cpp:43-61) falls back to 0 so it
+  // cannot poison the other pairs' sums.
   const double xs = P.cv_shift ? P.cv_shift[m] : 0.0;
-  const double ys = npairs > 0 ? pairs[(int64_t)idx[1] + (int64_t)idx[0] * n].x : 0.0;
+  const double y0 = npairs > 0 ? pairs[(int64_t)idx[1] + (int64_t)idx[0] * n].x : 0.0;
+  const double ys = isfinite(y0) ? y0 : 0.0;
 
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // n, sx, sy, sxx, syy, sxy, s(sign(x) y)
   // U: pairs in flight per thread (random 16-byte gathers)

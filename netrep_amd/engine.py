@@ -90,6 +90,14 @@ class Engine:
         self.n_nodes = n_nodes
         self.n_samples = n_samples if data_ptr else 0
 
+    def copy_dataset_from(self, other: "Engine"):
+        """Device-to-device copy of another context's resident dataset
+        (nr_copy_dataset: over xGMI between GPUs)."""
+        self._check(self._lib.nr_copy_dataset(self._h, other._h))
+        self.n_stat = other.n_stat
+        self.n_nodes = other.n_nodes
+        self.n_samples = other.n_samples
+
     def symmetric(self) -> bool:
         v = C.c_int()
         self._check(self._lib.nr_dataset_symmetric(self._h, C.byref(v)))

@@ -75,11 +75,38 @@ def extreme_counts(nulls, observed):
     return less, more, fin.sum(axis=2)
 
 
+def _align_vars_present(nVarsPresent, modules, n_rows):
+    """nVarsPresent by module label (R/pperm.R:106-111 requires
+    names(nVarsPresent) to match rownames(nulls)). A mapping (e.g.
+    contingencyTable's ``varsPres``) is aligned to ``modules`` by label; a
+    plain sequence is taken positionally."""
+    from collections.abc import Mapping
+    err = ValueError("expecting 'nVarsPresent' to be a numeric vector output by the "
+                     "'modulePreservation' function")
+    if isinstance(nVarsPresent, Mapping):
+        if modules is None:
+            raise ValueError("nVarsPresent given by module label: pass modules= (the row names of "
+                             "'nulls'/'observed')")
+        keys = [str(k) for k in nVarsPresent]
+        mods = [str(m) for m in modules]
+        if len(mods) != n_rows or sorted(keys) != sorted(mods):
+            raise err
+        lookup = {str(k): v for k, v in nVarsPresent.items()}
+        return [lookup[m] for m in mods]
+    vals = list(np.asarray(nVarsPresent).ravel())
+    if len(vals) != n_rows:
+        raise err
+    return vals
+
+
 def permutationTest(nulls, observed, nVarsPresent, totalSize, alternative="greater",
-                    statnames=None):
+                    statnames=None, modules=None):
     """R/pperm.R:74-167. nulls: (modules, statistics, permutations); observed:
-    (modules, statistics); nVarsPresent: per module; statnames: column names
-    of the statistics (defaults to the 7 or 4 of the reference)."""
+    (modules, statistics); nVarsPresent: per module, either a mapping
+    {module label: count} (contingencyTable's varsPres), aligned by label to
+    ``modules`` (the row names of nulls/observed), or a sequence in row order;
+    statnames: column names of the statistics (defaults to the 7 or 4 of the
+    reference)."""
     alts = ["two.sided", "less", "greater"]
     matches = [a for a in alts if a.startswith(alternative)]
     if len(matches) != 1:
@@ -89,6 +116,9 @@ def permutationTest(nulls, observed, nVarsPresent, totalSize, alternative="great
         raise ValueError("'totalSize' must be a single number > 0")
     nulls = np.asarray(nulls, dtype=np.float64)
     observed = np.asarray(observed, dtype=np.float64)
+    if nulls.ndim != 3 or observed.ndim != 2 or nulls.shape[:2] != observed.shape:
+        raise ValueError("mismatch in dimension names between 'nulls' and 'observed'")
+    nVarsPresent = _align_vars_present(nVarsPresent, modules, observed.shape[0])
     if statnames is None:
         statnames = STATNAMES if observed.shape[1] == 7 else ["avg.weight", "cor.cor", "cor.degree", "avg.cor"]
     less, more, n_ok = extreme_counts(nulls, observed)

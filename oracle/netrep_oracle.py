@@ -7,9 +7,15 @@ leg may import it. The product path (``netrep_amd``) never calls it.
 Every function restates one reference function formula by formula, citing
 the file:line it follows (paths relative to the reference tree). Where the
 reference delegates to third-party code that is absent here (Armadillo
-``svd_econ`` -> LAPACK ``dgesdd``; ``arma::cor``), the restatement calls the
-same LAPACK routine through scipy (``lapack_driver='gesdd'``) or the textbook
-definition (Pearson with n-1 normalisation).
+``svd_econ`` -> LAPACK; ``arma::cor``), the restatement calls the same
+LAPACK routine through scipy or the textbook definition (Pearson with n-1
+normalisation). ``svd_econ(U, S, V, X, "left", "dc")`` (src/netStats.cpp:229)
+takes Armadillo's divide-and-conquer branch only for mode "both"; for
+"left" it runs the standard driver ``dgesvd`` (JOBU='S', JOBVT='N'), so the
+restatement uses ``lapack_driver='gesvd'`` (``oracle/netrep_ref.cpp`` calls
+``dgesvd`` with exactly those job flags). tests/test_oracle_golden.py checks
+that gesvd and gesdd agree to 1e-12 on the golden cases, so fixtures made
+with either are interchangeable at the 1e-10 parity bar.
 
 Pinning: the observed 4x7 statistics and module-1 summary profiles printed
 in vignettes/NetRep.md:301-307 and :913-958 are reproduced by
@@ -31,6 +37,9 @@ import scipy.linalg
 STATNAMES = ["avg.weight", "coherence", "cor.cor", "cor.degree",
              "cor.contrib", "avg.cor", "avg.contrib"]          # src/permutations.cpp:174-177
 STATNAMES_NODATA = ["avg.weight", "cor.cor", "cor.degree", "avg.cor"]  # src/permutationsNoData.cpp:156-158
+
+# LAPACK driver behind arma::svd_econ(.., "left", "dc") (module docstring).
+SVD_DRIVER = "gesvd"
 
 # R's NA_real_: a quiet NaN whose low word is 1954.
 NA_REAL_BITS = np.uint64(0x7FF00000000007A2)
@@ -117,13 +126,14 @@ def corr_vector(corr, idx):
 
 
 def summary_profile(data, idx_sorted):
-    """SummaryProfile src/netStats.cpp:217-250: U[:,0] of svd_econ(X,'left','dc'), sign-oriented."""
+    """SummaryProfile src/netStats.cpp:217-250: U[:,0] of svd_econ(X,'left','dc')
+    (LAPACK dgesvd, see the module docstring), sign-oriented."""
     x = data[:, idx_sorted]
     s = data.shape[0]
     if not np.isfinite(x).all():               # svd_econ fails on non-finite input -> NaN (:231-235)
         return np.full(s, np.nan)
     try:
-        u, _, _ = scipy.linalg.svd(x, full_matrices=False, lapack_driver="gesdd",
+        u, _, _ = scipy.linalg.svd(x, full_matrices=False, lapack_driver=SVD_DRIVER,
                                    check_finite=False)
     except (np.linalg.LinAlgError, ValueError):
         return np.full(s, np.nan)

@@ -6,11 +6,14 @@
 // large cases on the GPU box and (2) as bench.py's `cpu_baseline` ("port"):
 // the same contiguous per-thread permutation chunks (src/permutations.cpp:
 // 338-354), one Fisher-Yates shuffle of the null pool per permutation (as
-// arma::shuffle, :63) when no explicit shuffle table is given, LAPACK dgesdd
-// for the summary profile (arma::svd_econ(..., "dc"), src/netStats.cpp:229),
-// single-threaded LAPACK per worker (R/modulePreservation.R:436-437).
-// LAPACK comes from scipy's bundled OpenBLAS (symbol scipy_dgesdd_), the only
-// LAPACK in this image; ref_init_lapack() loads it by path.
+// arma::shuffle, :63) when no explicit shuffle table is given, LAPACK dgesvd
+// with JOBU='S', JOBVT='N' for the summary profile -- what
+// arma::svd_econ(U, S, V, X, "left", "dc") (src/netStats.cpp:229) runs:
+// Armadillo takes its divide-and-conquer (dgesdd) branch only for mode
+// "both" -- and single-threaded LAPACK per worker
+// (R/modulePreservation.R:436-437). LAPACK comes from scipy's bundled
+// OpenBLAS (symbol scipy_dgesvd_), the only LAPACK in this image;
+// ref_init_lapack() loads it by path.
 //
 // Never linked into or called by the product (netrep_amd/).
 #include <dlfcn.h>
@@ -27,10 +30,10 @@
 
 namespace {
 
-typedef void (*dgesdd_t)(const char* jobz, const int* m, const int* n, double* a, const int* lda,
-                         double* s, double* u, const int* ldu, double* vt, const int* ldvt,
-                         double* work, const int* lwork, int* iwork, int* info);
-dgesdd_t g_dgesdd = nullptr;
+typedef void (*dgesvd_t)(const char* jobu, const char* jobvt, const int* m, const int* n, double* a,
+                         const int* lda, double* s, double* u, const int* ldu, double* vt,
+                         const int* ldvt, double* work, const int* lwork, int* info);
+dgesvd_t g_dgesvd = nullptr;
 std::string g_err;
 
 const double kNaN = std::numeric_limits<double>::quiet_NaN();
@@ -142,16 +145,17 @@ void profile(const double* data, int64_t S, const std::vector<int64_t>& srt, con
   if (!finite) return;  // svd_econ fails on non-finite input -> NaN summary
   std::vector<double> a = x;
   const int mn = std::min(m, n);
-  std::vector<double> s(mn), u((size_t)m * mn), vt((size_t)mn * n);
-  std::vector<int> iwork(8 * mn);
+  std::vector<double> s(mn), u((size_t)m * mn);
+  double vt_dummy = 0.0;
+  const int ldvt = 1;
   int lwork = -1, info = 0;
   double wq = 0.0;
-  const char jobz = 'S';
-  g_dgesdd(&jobz, &m, &n, a.data(), &m, s.data(), u.data(), &m, vt.data(), &mn, &wq, &lwork, iwork.data(), &info);
+  const char jobu = 'S', jobvt = 'N';  // auxlib::svd_econ(U, S, V, A, 'l')
+  g_dgesvd(&jobu, &jobvt, &m, &n, a.data(), &m, s.data(), u.data(), &m, &vt_dummy, &ldvt, &wq, &lwork, &info);
   lwork = (int)wq + 1;
   std::vector<double> work(lwork);
-  g_dgesdd(&jobz, &m, &n, a.data(), &m, s.data(), u.data(), &m, vt.data(), &mn, work.data(), &lwork,
-           iwork.data(), &info);
+  g_dgesvd(&jobu, &jobvt, &m, &n, a.data(), &m, s.data(), u.data(), &m, &vt_dummy, &ldvt, work.data(), &lwork,
+           &info);
   if (info != 0) return;
   std::vector<double> sp(u.begin(), u.begin() + m);
   std::vector<double> mo(m, 0.0);
@@ -222,9 +226,9 @@ const char* ref_last_error() { return g_err.c_str(); }
 int ref_init_lapack(const char* so_path) {
   void* h = dlopen(so_path, RTLD_NOW | RTLD_LOCAL);
   if (!h) { g_err = dlerror(); return 1; }
-  g_dgesdd = (dgesdd_t)dlsym(h, "scipy_dgesdd_");
-  if (!g_dgesdd) g_dgesdd = (dgesdd_t)dlsym(h, "dgesdd_");
-  if (!g_dgesdd) { g_err = "no dgesdd symbol"; return 1; }
+  g_dgesvd = (dgesvd_t)dlsym(h, "scipy_dgesvd_");
+  if (!g_dgesvd) g_dgesvd = (dgesvd_t)dlsym(h, "dgesvd_");
+  if (!g_dgesvd) { g_err = "no dgesvd symbol"; return 1; }
   typedef void (*setthreads_t)(int);
   setthreads_t st = (setthreads_t)dlsym(h, "scipy_openblas_set_num_threads");
   if (st) st(1);  // BLAS threads forced to 1 (R/modulePreservation.R:433-437)
@@ -240,7 +244,7 @@ int ref_permutation_procedure(const double* data, const double* corr, const doub
                               const int32_t* null_idx, int64_t n_null, const double* disc_cv,
                               const double* disc_wd, const double* disc_nc, int64_t n_perm, uint64_t seed,
                               const uint32_t* pi, int n_threads, double* nulls, double* observed) {
-  if (data && !g_dgesdd) { g_err = "LAPACK not initialised"; return 1; }
+  if (data && !g_dgesvd) { g_err = "LAPACK not initialised"; return 1; }
   Problem P{data, corr, net, N, S, n_rows, n_present, row_of, test_idx, null_pos, null_idx, node_off,
             n_null, disc_cv, disc_wd, disc_nc, data ? 7 : 4, {}};
   P.cv_off.assign(n_present + 1, 0);

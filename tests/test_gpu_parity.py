@@ -251,7 +251,7 @@ def test_constant_column_gives_na():
 def test_large_modules_vs_cpp_oracle(seed):
     """C3-like module sizes (k up to 300, S = 200) on a 4,000-node dataset:
     the Lanczos eigen-solver path at the sizes the benchmark runs, checked
-    against the C++ restatement (LAPACK dgesdd) on identical shuffles."""
+    against the C++ restatement (LAPACK dgesvd) on identical shuffles."""
     from netrep_amd import synthetic as S
     from oracle import ref_cpp
     sizes = [300, 260, 200, 150, 90, 40, 31]
@@ -281,7 +281,7 @@ def test_c5_sized_modules_vs_cpp_oracle():
     """C5-shaped modules (BASELINE configs[4]: up to 2,000 nodes at S = 1,000,
     so k > S): the large-module layout (full Gram, matvec partials in global
     scratch, 320-vector Lanczos basis, network statistics as their own
-    kernel) against the C++ restatement (LAPACK dgesdd) on identical shuffles,
+    kernel) against the C++ restatement (LAPACK dgesvd) on identical shuffles,
     observed values through IntermediateProperties-shaped discovery vectors."""
     from netrep_amd import synthetic as S
     from oracle import ref_cpp

@@ -66,8 +66,12 @@ def test_contingency_partial_overlap_and_test_modules():
     disc = {f"N_{i}": str(1 + i % 3) for i in range(1, 13)}
     test_nodes = [f"N_{i}" for i in range(1, 13, 2)] + ["X_1"]
     test = {n: ("a" if i % 2 else "b") for i, n in enumerate(test_nodes)}
-    ct = CT.contingencyTable([disc, test], ["1", "2", "3", "7"], test_nodes)
-    assert ct["varsPres"]["7"] == 0
+    # a requested module with no discovery node: varsPres 0, propVarsPres NA
+    # without test assignments; with them R fails at contingency[mods,,]
+    # (R/contingency.R:95), as test_contingency_module_absent_from_discovery checks
+    ct7 = CT.contingencyTable([disc, None], ["1", "2", "3", "7"], test_nodes)
+    assert ct7["varsPres"]["7"] == 0 and np.isnan(ct7["propVarsPres"]["7"])
+    ct = CT.contingencyTable([disc, test], ["1", "2", "3"], test_nodes)
     assert sum(ct["varsPres"].values()) == 6
     mat, rows, cols = ct["contingency"]
     assert rows[:2] == ["size", "present"] and cols[:2] == ["size", "present"]
@@ -83,3 +87,39 @@ def test_bench_traffic_lookup_matches_committed_pmc():
     assert t is not None and t > 0
     assert bench.measured_traffic("C3", 512, "module_profile_kernel") is None
     assert bench.measured_traffic("C2", 256, "module_profile_kernel") is None
+
+
+def test_vars_present_aligned_by_label_from_contingency():
+    """contingencyTable's varsPres (ordered by orderAsNumeric) chained
+    into permutationTest with rows in another order: counts follow the labels,
+    a label mismatch raises the reference's error (R/pperm.R:106-111)."""
+    from netrep_amd.contingency import contingencyTable
+    ma = {f"n{i}": lab for i, lab in enumerate(["10"] * 5 + ["2"] * 3 + ["0"] * 4)}
+    ct = contingencyTable([ma, None], ["10", "2"], list(ma))
+    assert list(ct["varsPres"]) == ["2", "10"]            # orderAsNumeric
+    rng = np.random.default_rng(3)
+    nulls = rng.standard_normal((2, 7, 200))
+    obs = rng.standard_normal((2, 7))
+    rows = ["10", "2"]
+    got = PV.permutationTest(nulls, obs, ct["varsPres"], 12, "greater", modules=rows)
+    exp = PV.permutationTest(nulls, obs, [5, 3], 12, "greater")
+    np.testing.assert_array_equal(got, exp)
+    with pytest.raises(ValueError, match="nVarsPresent"):
+        PV.permutationTest(nulls, obs, ct["varsPres"], 12, "greater", modules=["10", "7"])
+    with pytest.raises(ValueError, match="modules="):
+        PV.permutationTest(nulls, obs, ct["varsPres"], 12, "greater")
+
+
+def test_order_as_numeric_follows_r_as_integer():
+    from netrep_amd.contingency import order_as_numeric
+    assert order_as_numeric(["10", "2", "1.0", "1e1"]) == ["1.0", "2", "10", "1e1"]
+    assert order_as_numeric(["b", "10", "a"]) == ["10", "a", "b"]      # as.integer warns -> character order
+
+
+def test_contingency_module_absent_from_discovery():
+    from netrep_amd.contingency import contingencyTable
+    ma = {"a": "1", "b": "1", "c": "2"}
+    ct = contingencyTable([ma, None], ["1", "3"], ["a", "b", "c"])
+    assert ct["varsPres"]["3"] == 0 and np.isnan(ct["propVarsPres"]["3"])
+    with pytest.raises(ValueError, match="subscript out of bounds"):
+        contingencyTable([ma, {"a": "x", "b": "y", "c": "x"}], ["1", "3"], ["a", "b", "c"])

@@ -118,3 +118,28 @@ def test_sign_and_na_semantics():
     na = O.na_fill([np.nan, np.inf, 1.0])
     assert na.view(np.uint64)[0] == O.NA_REAL_BITS and na.view(np.uint64)[1] == O.NA_REAL_BITS
     assert np.isnan(O.average_edge_weight(np.array([0.0])))  # k = 1 -> 0/0
+
+
+def test_svd_driver_gesvd_agrees_with_gesdd(bundled, asym):
+    """arma::svd_econ(.., "left", "dc") runs dgesvd (Armadillo uses dgesdd only
+    for mode "both"); the oracle follows it. Either driver's sign-oriented top
+    left singular vector -- and so every summary-profile statistic -- agrees to
+    1e-12 on the golden cases, so fixtures made with dgesdd stay valid."""
+    import scipy.linalg
+    cases = []
+    b = bundled
+    for key in ("discovery_data", "test_data"):
+        x = O.scale(b[key])
+        rng = np.random.default_rng(1)
+        for k in (20, 35, 60):
+            cases.append(x[:, np.sort(rng.choice(x.shape[1], k, replace=False))])
+    xa = O.scale(asym["t_data"])
+    cases.append(xa[:, :14])
+    for x in cases:
+        us = []
+        for drv in ("gesvd", "gesdd"):
+            u = scipy.linalg.svd(x, full_matrices=False, lapack_driver=drv)[0][:, 0]
+            c = np.corrcoef(x.mean(axis=1), u)[0, 1]
+            us.append(-u if c < 0 else u)
+        assert np.abs(us[0] - us[1]).max() <= 1e-12
+    assert O.SVD_DRIVER == "gesvd"
