@@ -119,11 +119,7 @@ def setup_dist(args):
     return world, rank, local
 
 
-def scale_rows(x):
-    """Scale (src/scale.cpp:21) applied to genes stored as rows of x (N x S)."""
-    mu = x.mean(dim=1, keepdim=True)
-    sd = x.std(dim=1, unbiased=True, keepdim=True)
-    return (x - mu) / sd
+scale_rows = S.scale_rows_torch
 
 
 def build_case(cfg, world, rank, local, seed):
@@ -141,6 +137,9 @@ def build_case(cfg, world, rank, local, seed):
     if rank == 0:
         dx, dc, dn = S.torch_dataset(lay, n_samples, seed + 1, device=dev)
         dxs = scale_rows(dx).contiguous()
+        # torch's stream belongs to its own HIP runtime, not ordered with the
+        # engine's: the inputs must be complete before the engine reads them
+        torch.cuda.synchronize()
         eng.set_dataset_device(dc.data_ptr(), dn.data_ptr(), dxs.data_ptr() if with_data else 0,
                                n_nodes, n_samples)
         del dx, dc, dn, dxs
@@ -168,6 +167,7 @@ def build_case(cfg, world, rank, local, seed):
         broadcast_tensors([tc, tn, txs], src=0)   # RCCL over xGMI
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - t0
+    torch.cuda.synchronize()
     eng.set_dataset_device(tc.data_ptr(), tn.data_ptr(), txs.data_ptr() if with_data else 0,
                            n_nodes, n_samples)
     eng.set_modules(len(mods), np.arange(len(mods)), node_off, idx, idx,  # null pool = all genes

@@ -99,6 +99,24 @@ SIGNATURES = {
 _lib = None
 
 
+def _init_torch_runtime_first() -> None:
+    """PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so, a
+    different soname from /opt/rocm's libamdhip64.so.7 this library links),
+    so a process that uses both holds two runtimes. Measured on MI355X: torch
+    initialised AFTER the engine's runtime sees no device, the reverse order
+    works (bench.py passes torch-allocated device buffers to the engine). So
+    when torch is installed its runtime is initialised before the engine
+    library loads; without torch this is a no-op."""
+    try:
+        import torch
+    except ImportError:
+        return
+    try:
+        torch.cuda.is_available()
+    except Exception:  # pragma: no cover - a broken torch install must not block the engine
+        pass
+
+
 def load() -> C.CDLL:
     """Load (once) and return the engine library; raise if it is missing."""
     global _lib
@@ -107,6 +125,7 @@ def load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise NetRepError(NR_ERR_INVALID,
                           f"engine library not built: {LIB_PATH} (run __graft_entry__.build())")
+    _init_torch_runtime_first()
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

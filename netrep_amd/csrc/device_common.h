@@ -1,0 +1,536 @@
+// Device helpers shared by the engine's kernels (kernels.hip, kernels_rg4.hip):
+// wave/block reductions, R's NA_real_, the index source of a permuted module
+// (GetRandomIdx, src/utils.cpp:193-199), CorrVector pair decoding, register
+// butterflies on gfx950 (permlane swaps, DPP), the Lanczos tridiagonal
+// helpers (top eigenvalue / residual / eigenvector, partial
+// reorthogonalisation's omega recurrence) and diagnostic phase stamps.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "prp.h"
+#include "kernels.h"
+
+namespace nr {
+
+#define NR_BS 256
+#define NR_WAVES (NR_BS / 64)
+
+__device__ __forceinline__ double nr_nan() { return __longlong_as_double(0x7FF8000000000000ll); }
+
+// R's NA_real_ (src/permutations.cpp:383-384 fills non-finite with NA_REAL).
+__device__ __forceinline__ double na_fill(double x) {
+  return isfinite(x) ? x : __longlong_as_double(0x7FF00000000007A2ll);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sums of N values; result broadcast to every thread. `red` must
+// hold N * NR_WAVES doubles of LDS. Contains two barriers.
+template <int N, int NW = NR_WAVES>
+__device__ __forceinline__ void block_sums(double (&v)[N], double* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) red[i * NW + wave] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[i * NW + w];
+    v[i] = s;
+  }
+  __syncthreads();
+}
+
+// Pearson correlation from (shifted) one-pass sums over complete cases.
+__device__ __forceinline__ double pearson_sums(double n, double sx, double sy,
+                                               double sxx, double syy, double sxy) {
+  if (n < 1.0) return nr_nan();
+  const double cov = sxy - sx * sy / n;
+  const double vx = sxx - sx * sx / n;
+  const double vy = syy - sy * sy / n;
+  return cov / (sqrt(vx) * sqrt(vy));
+}
+
+// Test column of module node c of item (p, m): GetRandomIdx
+// (src/utils.cpp:193-199) under a PRP, an explicit table, or a direct set.
+__device__ __forceinline__ uint32_t node_index(const IndexSource& src, const nr_prp_key& key,
+                                               int64_t p_local, int64_t node) {
+  if (src.mode == NR_IDX_DIRECT) return (uint32_t)src.direct_idx[node];
+  const uint32_t q = (uint32_t)src.null_pos[node];
+  const uint32_t s = (src.mode == NR_IDX_PRP)
+                         ? nr_prp_permute(key, q)
+                         : src.pi[p_local * (int64_t)src.n_null + q];
+  return (uint32_t)src.null_idx[s];
+}
+
+// Decode flat CorrVector position v -> (jj, ii), ii > jj, column-major lower
+// triangle (src/netStats.cpp:196-201).
+__device__ __forceinline__ void decode_pair(int64_t v, int64_t k, int64_t& jj, int64_t& ii) {
+  const double b = (double)(2 * k - 1);
+  int64_t j = (int64_t)floor((b - sqrt(b * b - 8.0 * (double)v)) * 0.5);
+  if (j < 0) j = 0;
+  // off(j) = j*(2k-j-1)/2 pairs precede column j
+  while (j > 0 && j * (2 * k - j - 1) / 2 > v) --j;
+  while ((j + 1) * (2 * k - j - 2) / 2 <= v) ++j;
+  jj = j;
+  ii = v - j * (2 * k - j - 1) / 2 + j + 1;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2: summary-profile statistics. Persistent workgroups pull items from
+// a queue; each owns a scratch slot holding G = X^T X and the Lanczos basis.
+// ---------------------------------------------------------------------------
+typedef double nr_f64x4 __attribute__((ext_vector_type(4)));
+
+// 1/d: v_rcp_f64 refined by two Newton steps as in the compiler's own
+// division expansion, without its scaling/fixup (d normal, |d| >= 1e-300);
+// used only in the Sturm counts of the Ritz checks.
+__device__ __forceinline__ double nr_rcp(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+}
+
+// Largest eigenvalue of the symmetric tridiagonal (alpha[0..n), beta[0..n-1))
+// by 64-way multisection on Sturm counts; executed by one full wave. The
+// counts use the characteristic-polynomial recurrence of the Gershgorin-
+// normalised matrix, p_i = (a_i - x) p_{i-1} - b_{i-1}^2 p_{i-2} (sign changes
+// of p_0..p_n = eigenvalues below x): one FMA on the dependency chain per
+// step and no division; |p| is renormalised every 4 steps.
+static __device__ double tri_top_eigenvalue(const double* alpha, const double* beta, int n, int lane) {
+  double lo = alpha[0], hi = alpha[0];
+  for (int i = lane; i < n; i += 64) {
+    const double r = (i > 0 ? fabs(beta[i - 1]) : 0.0) + (i < n - 1 ? fabs(beta[i]) : 0.0);
+    lo = fmin(lo, alpha[i] - r);
+    hi = fmax(hi, alpha[i] + r);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  const double scale = fmax(fabs(lo), fabs(hi)) + 1e-300;
+  const double inv = 1.0 / scale;
+  lo -= 1e-14 * scale;
+  hi += 1e-14 * scale;
+  for (int it = 0; it < 12; ++it) {
+    const double x = (lo + (hi - lo) * (double)(lane + 1) / 65.0) * inv;
+    double p0 = 1.0, p1 = alpha[0] * inv - x;
+    int cnt = p1 < 0.0;  // eigenvalues < x
+#pragma unroll 4
+    for (int i = 1; i < n; ++i) {
+      const double b = beta[i - 1] * inv;
+      const double p2 = fma(alpha[i] * inv - x, p1, -(b * b) * p0);
+      cnt += (p2 < 0.0) != (p1 < 0.0);
+      p0 = p1;
+      p1 = p2;
+      if ((i & 3) == 0) {
+        const double mg = fabs(p1);
+        const double s = mg > 1e150 ? 1e-150 : (mg < 1e-150 ? 1e150 : 1.0);
+        p0 *= s;
+        p1 *= s;
+      }
+    }
+    // largest x with cnt <= n-1 becomes lo; smallest x with cnt == n becomes hi
+    const unsigned long long below = __ballot(cnt <= n - 1);
+    // lanes are ordered by x: lanes [0, t) have cnt <= n-1, lanes [t, 64) have cnt == n
+    const int t = __popcll(below);
+    const double xlo = lo + (hi - lo) * (double)t / 65.0;
+    const double xhi = lo + (hi - lo) * (double)(t + 1) / 65.0;
+    lo = xlo;
+    hi = xhi;
+    if (hi - lo <= 2e-16 * scale) break;
+  }
+  return 0.5 * (lo + hi);
+}
+
+// Convergence estimate of the top Ritz pair: |last component| of the unit
+// eigenvector y of the tridiagonal for theta, times beta_j. y comes from the
+// three-term recurrence run BACKWARDS from y_{n-1} = 1: the top eigenvector
+// of an unreduced Jacobi matrix is positive and its tail decays once the
+// pair converges, so upward it is the dominant (stable) solution. rb holds
+// 1/beta[0..n-1), one wave fills it. Returns beta_j / |y| (lane 0).
+static __device__ double tri_top_resid(const double* alpha, const double* beta, int n, double theta, double beta_j,
+                                double* rb, int lane) {
+  for (int i = lane; i < n - 1; i += 64) rb[i] = 1.0 / beta[i];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  double y1 = 1.0, y2 = 0.0, ss = 1.0;  // y_i, y_{i+1}, sum of squares
+  for (int i = n - 1; i > 0; --i) {
+    const double y0 = fma(theta - alpha[i], y1, -(i < n - 1 ? beta[i] : 0.0) * y2) * rb[i - 1];
+    ss = fma(y0, y0, ss);
+    y2 = y1;
+    y1 = y0;
+    if (ss > 1e200) {
+      y1 *= 1e-100;
+      y2 *= 1e-100;
+      ss *= 1e-200;
+      beta_j *= 1e-100;
+    }
+  }
+  return beta_j / sqrt(ss);
+}
+
+// Eigenvector of the tridiagonal for eigenvalue theta by two steps of inverse
+// iteration; LU with partial pivoting as LAPACK dgttrf/dgtts2. Single lane.
+// y[0..n) comes back normalised; work holds 5n doubles.
+static __device__ void tri_eigenvector(const double* alpha, const double* beta, int n, double theta,
+                                double* y, double* work) {
+  double* dl = work;
+  double* d = work + n;
+  double* du = work + 2 * n;
+  double* du2 = work + 3 * n;
+  double* swp = work + 4 * n;
+  double scale = fabs(theta);
+  for (int i = 0; i < n; ++i) {
+    d[i] = alpha[i] - theta;
+    scale = fmax(scale, fabs(alpha[i]));
+    if (i < n - 1) {
+      du[i] = beta[i];
+      dl[i] = beta[i];
+      scale = fmax(scale, fabs(beta[i]));
+    }
+    du2[i] = 0.0;
+    swp[i] = 0.0;
+  }
+  const double floor_piv = 1e-300 + 2.2e-16 * scale;
+  for (int i = 0; i < n - 1; ++i) {
+    if (fabs(d[i]) >= fabs(dl[i])) {
+      if (fabs(d[i]) < floor_piv) d[i] = d[i] < 0.0 ? -floor_piv : floor_piv;
+      const double f = dl[i] / d[i];
+      dl[i] = f;
+      d[i + 1] -= f * du[i];
+    } else {
+      const double f = d[i] / dl[i];
+      d[i] = dl[i];
+      dl[i] = f;
+      const double t = du[i];
+      du[i] = d[i + 1];
+      d[i + 1] = t - f * d[i + 1];
+      if (i < n - 2) {
+        du2[i] = du[i + 1];
+        du[i + 1] = -f * du[i + 1];
+      }
+      swp[i] = 1.0;
+    }
+  }
+  if (fabs(d[n - 1]) < floor_piv) d[n - 1] = d[n - 1] < 0.0 ? -floor_piv : floor_piv;
+  for (int i = 0; i < n; ++i) y[i] = 1.0;
+  for (int iter = 0; iter < 2; ++iter) {
+    for (int i = 0; i < n - 1; ++i) {
+      if (swp[i] == 0.0) {
+        y[i + 1] -= dl[i] * y[i];
+      } else {
+        const double t = y[i];
+        y[i] = y[i + 1];
+        y[i + 1] = t - dl[i] * y[i];
+      }
+    }
+    y[n - 1] /= d[n - 1];
+    if (n > 1) y[n - 2] = (y[n - 2] - du[n - 2] * y[n - 1]) / d[n - 2];
+    for (int i = n - 3; i >= 0; --i) y[i] = (y[i] - du[i] * y[i + 1] - du2[i] * y[i + 2]) / d[i];
+    double mx = 0.0;
+    for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(y[i]));
+    double nrm = 0.0;
+    for (int i = 0; i < n; ++i) {
+      y[i] /= mx;
+      nrm += y[i] * y[i];
+    }
+    const double inv = 1.0 / sqrt(nrm);
+    for (int i = 0; i < n; ++i) y[i] *= inv;
+  }
+}
+
+// Partial reorthogonalisation (Simon 1984): omega_{j+1,i} estimates q_{j+1}.q_i
+// from the recurrence on T's entries; run by one wave over i = 0..j. Returns
+// max_i |omega_{j+1,i}| (all lanes). om_cur = omega_{j,.}, om_prev = omega_{j-1,.}.
+__device__ __forceinline__ double omega_update(const double* alpha, const double* beta, int j, double beta_j,
+                                               const double* om_cur, const double* om_prev, double* om_next,
+                                               double anorm, int k, int lane) {
+  const double eps = 2.220446049250313e-16;
+  const double psi = eps * anorm / beta_j;
+  double mx = 0.0;
+  for (int i = lane; i < j; i += 64) {
+    double t = beta[i] * om_cur[i + 1] + (alpha[i] - alpha[j]) * om_cur[i] -
+               (j > 0 ? beta[j - 1] * om_prev[i] : 0.0);
+    if (i > 0) t += beta[i - 1] * om_cur[i - 1];
+    t = t / beta_j;
+    t += t >= 0.0 ? psi : -psi;
+    om_next[i] = t;
+    mx = fmax(mx, fabs(t));
+  }
+  if (lane == 0) {
+    om_next[j] = eps * sqrt((double)k) * anorm / beta_j;
+    om_next[j + 1] = 1.0;
+    mx = fmax(mx, fabs(om_next[j]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+  return mx;
+}
+
+// Cross-lane butterfly steps without LDS (gfx950): v_permlane32_swap /
+// v_permlane16_swap exchange half-waves / odd-even rows of two registers, so
+// x' + y' leaves lanes [0,32) with x summed over the lane pair (l, l^32) and
+// lanes [32,64) with y summed likewise (16-lane rows for the 16 variant).
+__device__ __forceinline__ double nr_swap32_sum(double x, double y) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(y), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(y), false, false);
+  return __hiloint2double((int)hi[0], (int)lo[0]) + __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ double nr_swap16_sum(double x, double y) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(y), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(y), false, false);
+  return __hiloint2double((int)hi[0], (int)lo[0]) + __hiloint2double((int)hi[1], (int)lo[1]);
+}
+// DPP lane moves within 16-lane rows (both dwords of a double).
+template <int CTRL>
+__device__ __forceinline__ double nr_dpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+constexpr int NR_DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int NR_DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int NR_DPP_ROR8 = 0x128;        // row_ror:8 == lane ^ 8 within a row
+constexpr int NR_DPP_HALF_MIRROR = 0x141; // lane ^ 7 within 8 lanes (flips bit 2)
+
+// Transpose-reduce of 16 per-lane column partials up[0..16) over the 64 rows
+// (lanes) of a unit: afterwards lanes with (lane & 3) == 0 hold the column
+// sum of column 8*b5 + 4*b4 + 2*b3 + b2 (b = lane bits). 8 + 4 swaps, 3 + 2
+// DPP-exchange levels; no LDS traffic.
+__device__ __forceinline__ double nr_transpose_reduce16(const double (&up)[16], int lane) {
+  double a8[8], a4[4], a2[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a8[i] = nr_swap32_sum(up[i], up[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a4[i] = nr_swap16_sum(a8[i], a8[i + 4]);
+  const bool b3 = lane & 8;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    a2[i] = (b3 ? a4[i + 2] : a4[i]) + nr_dpp<NR_DPP_ROR8>(b3 ? a4[i] : a4[i + 2]);
+  const bool b2 = lane & 4;
+  double v = (b2 ? a2[1] : a2[0]) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? a2[0] : a2[1]);
+  v += nr_dpp<NR_DPP_XOR2>(v);
+  v += nr_dpp<NR_DPP_XOR1>(v);
+  return v;
+}
+
+// Phase stamps (diagnostics only: active when P.stamps != NULL, a separate
+// measurement run; no stamp executes otherwise). Thread 0 accumulates shader
+// cycles per phase between the barriers that already delimit the phases.
+__device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memtime(); }
+#define NR_STAMP(slot)                                                          \
+  do {                                                                          \
+    if (P.stamps && threadIdx.x == 0) {                                         \
+      const uint64_t t_ = nr_clock();                                           \
+      atomicAdd((unsigned long long*)&P.stamps[slot], (unsigned long long)(t_ - t_mark)); \
+      t_mark = t_;                                                              \
+    }                                                                           \
+  } while (0)
+
+// Sum of a[r] over lane bits 0..3 (the 16 columns of a tile); lanes with
+// (lane & 3) == 0 end with the total of row group r = 2*b3 + b2, i.e. tile
+// row (lane >> 4) + 4r.
+__device__ __forceinline__ double rg_row_reduce(const double (&a)[4], int lane) {
+  const bool b3 = lane & 8, b2 = lane & 4;
+  const double v0 = (b3 ? a[2] : a[0]) + nr_dpp<NR_DPP_ROR8>(b3 ? a[0] : a[2]);
+  const double v1 = (b3 ? a[3] : a[1]) + nr_dpp<NR_DPP_ROR8>(b3 ? a[1] : a[3]);
+  double v = (b2 ? v1 : v0) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? v0 : v1);
+  v += nr_dpp<NR_DPP_XOR2>(v);
+  v += nr_dpp<NR_DPP_XOR1>(v);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Summary-profile item pipeline pieces shared by every Gram storage scheme:
+// LDS carve-out, node contributions from the Ritz vector, the statistics, and
+// the persistent work queue.
+// ---------------------------------------------------------------------------
+
+// LDS carve-out common to all summary-profile bodies.
+struct LzLds {
+  double *red, *q, *qprev, *w, *vv, *gv, *colm;
+  double *alpha, *beta, *h, *ty, *twork, *omg;
+  uint32_t* idx;
+  int mmax;
+};
+
+// Carves red, q, qprev, w, vv, gv, colm (kvec each), then `extra` doubles for
+// the storage scheme (returned in *extra_out), then the Lanczos tridiagonal
+// arrays and idx. Layout matches profile_kernel_lds / reg_kernel_lds.
+template <int NW>
+__device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mmax, int64_t extra,
+                                           double** extra_out) {
+  LzLds L;
+  L.red = reinterpret_cast<double*>(smem);  // 8 * NW
+  L.q = L.red + 8 * NW;
+  L.qprev = L.q + kvec;
+  L.w = L.qprev + kvec;
+  L.vv = L.w + kvec;
+  L.gv = L.vv + kvec;
+  L.colm = L.gv + kvec;
+  *extra_out = L.colm + kvec;
+  L.alpha = *extra_out + extra;  // [mmax]
+  L.beta = L.alpha + mmax;       // [mmax]
+  L.h = L.beta + mmax;           // [mmax]
+  L.ty = L.h + mmax;             // [mmax]
+  L.twork = L.ty + mmax;         // [5 * mmax]
+  L.omg = L.twork + 5 * mmax;    // [3 * (mmax + 1)] omega rows
+  L.idx = reinterpret_cast<uint32_t*>(L.omg + 3 * (mmax + 1));  // [kvec]
+  L.mmax = mmax;
+  return L;
+}
+
+// Node contributions from the Ritz vector (u = X v / sigma):
+//   NC_j = cor(x_j, u) = ((Gv)_j/sigma - S m_j ubar) / sqrt((G_jj - S m_j^2)(1 - S ubar^2)),
+// oriented by sign(cor(rowMeans(X), u)) (src/netStats.cpp:242-247, 279); the
+// result goes to L.w. diag(c) = G_cc; L.colm holds the column means.
+template <int NW, class MV, class DG>
+__device__ __forceinline__ void profile_contrib(const ProfileParams& P, int k, int m, const LzLds& L,
+                                                const double* __restrict__ X, int S, double ones_g_ones,
+                                                MV& mv, DG diag) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x;
+  const double Sd = (double)S;
+  double* vv = L.vv;
+  double* gv = L.gv;
+  double* colm = L.colm;
+  mv(vv, gv, nullptr);
+  // lambda = v.Gv; ubar = mean of u = X v / sigma
+  double a3[2] = {0.0, 0.0};
+  for (int c = tid; c < k; c += BS) {
+    a3[0] += vv[c] * gv[c];
+    a3[1] += colm[c] * vv[c];
+  }
+  block_sums<2, NW>(a3, L.red);
+  const double lambda = a3[0];
+  const double sigma = sqrt(lambda);
+  const double ubar = a3[1] / sigma;
+  const double var_u = 1.0 - Sd * ubar * ubar;  // sum (u - ubar)^2 with |u| = 1
+  // orientation: sign(cor(meanObs, u)) (src/netStats.cpp:242-247); the sign
+  // of the covariance is that of sum_j cov(x_j, u); var(meanObs) * k^2 * (S-1)
+  // = 1'G1 - (sum of all data)^2 / S.
+  double a4[2] = {0.0, 0.0};
+  for (int c = tid; c < k; c += BS) {
+    a4[0] += gv[c] / sigma - Sd * colm[c] * ubar;
+    a4[1] += colm[c];
+  }
+  block_sums<2, NW>(a4, L.red);
+  const double var_mo = ones_g_ones - Sd * a4[1] * a4[1];
+  const bool flip = (a4[0] < 0.0) && (var_mo > 0.0) && (var_u > 0.0);
+  const double sgn = flip ? -1.0 : 1.0;
+  // NC_j = cor(x_j, u) (src/netStats.cpp:279); node order = CSR order
+  for (int c = tid; c < k; c += BS) {
+    const double cov = gv[c] / sigma - Sd * colm[c] * ubar;
+    const double var_x = diag(c) - Sd * colm[c] * colm[c];
+    L.w[c] = sgn * cov / (sqrt(var_x) * sqrt(var_u));
+  }
+  if (P.sp_out) {
+    for (int r = tid; r < S; r += BS) {
+      double s = 0.0;
+      for (int c = 0; c < k; ++c) s += X[(int64_t)L.idx[c] * S + r] * vv[c];
+      P.sp_out[(int64_t)m * S + r] = sgn * s / sigma;
+    }
+  }
+  __syncthreads();
+}
+
+// svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235).
+template <int NW>
+__device__ __forceinline__ void profile_nonfinite(const ProfileParams& P, int k, int m, int S, const LzLds& L) {
+  constexpr int BS = NW * 64;
+  for (int c = threadIdx.x; c < k; c += BS) L.w[c] = nr_nan();
+  if (P.sp_out)
+    for (int r = threadIdx.x; r < S; r += BS) P.sp_out[(int64_t)m * S + r] = nr_nan();
+  __syncthreads();
+}
+
+// ModuleCoherence (src/netStats.cpp:293-305), Correlation / SignAwareMean
+// against the discovery contribution (src/permutations.cpp:99,101); node
+// contributions in L.w.
+template <int NW>
+__device__ __forceinline__ void profile_stats(const ProfileParams& P, int k, int m, int64_t off,
+                                              int64_t p_local, const LzLds& L) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x;
+  const double* w = L.w;
+  double b1[5] = {0, 0, 0, 0, 0};  // nfinite, sum nc^2, ncc, sx, sy
+  for (int c = tid; c < k; c += BS) {
+    const double y = w[c];
+    if (isfinite(y)) { b1[0] += 1.0; b1[1] += y * y; }
+    if (P.disc_nc) {
+      const double xv = P.disc_nc[off + c];
+      if (isfinite(xv) && isfinite(y)) { b1[2] += 1.0; b1[3] += xv; b1[4] += y; }
+    }
+    if (P.nc_out) P.nc_out[off + c] = y;
+  }
+  block_sums<5, NW>(b1, L.red);
+  const double stat_coh = b1[0] >= 1.0 ? b1[1] / b1[0] : nr_nan();
+  double stat_cc = nr_nan(), stat_ac = nr_nan();
+  if (P.disc_nc && P.out) {
+    const double mx = b1[3] / b1[2], my = b1[4] / b1[2];
+    double b2[4] = {0, 0, 0, 0};
+    for (int c = tid; c < k; c += BS) {
+      const double y = w[c], xv = P.disc_nc[off + c];
+      if (isfinite(xv) && isfinite(y)) {
+        const double dx = xv - mx, dy = y - my;
+        b2[0] += dx * dx;
+        b2[1] += dy * dy;
+        b2[2] += dx * dy;
+        b2[3] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
+      }
+    }
+    block_sums<4, NW>(b2, L.red);
+    stat_cc = b1[2] >= 1.0 ? b2[2] / (sqrt(b2[0]) * sqrt(b2[1])) : nr_nan();
+    stat_ac = b1[2] >= 1.0 ? b2[3] / b1[2] : nr_nan();
+  }
+  if (tid == 0) {
+    if (P.out) {
+      double* o = P.out + (int64_t)P.row_of[m] + (int64_t)P.n_rows * (int64_t)P.n_stat * p_local;
+      o[(int64_t)P.n_rows * P.slot_coherence] = na_fill(stat_coh);
+      o[(int64_t)P.n_rows * P.slot_cor_contrib] = na_fill(stat_cc);
+      o[(int64_t)P.n_rows * P.slot_avg_contrib] = na_fill(stat_ac);
+    }
+    if (P.coh_out) P.coh_out[m] = stat_coh;
+  }
+  __syncthreads();
+}
+
+// Next item from the persistent queue: (module m, local permutation, CSR
+// offset, k) and its index set in L.idx. Returns false when drained.
+template <int NW>
+__device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L, int* flags, int& m,
+                                          int64_t& p_local, int64_t& off, int& k) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x;
+  if (tid == 0) flags[0] = atomicAdd(P.queue, 1);
+  __syncthreads();
+  const int item = flags[0];
+  __syncthreads();
+  if (item >= P.n_items) return false;
+  const int64_t mslot = item / P.n_perm;
+  p_local = item - mslot * P.n_perm;
+  m = P.mod_order[mslot];
+  off = P.node_off[m];
+  k = (int)(P.node_off[m + 1] - off);
+  nr_prp_key key;
+  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
+  for (int c = tid; c < k; c += BS) L.idx[c] = node_index(P.src, key, p_local, off + c);
+  if (tid == 0) flags[1] = 0;
+  __syncthreads();
+  return true;
+}
+}  // namespace nr

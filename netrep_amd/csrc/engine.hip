@@ -81,7 +81,6 @@ struct nr_ctx {
   size_t stage_cap = 0;
   uint32_t* d_pi = nullptr;
   size_t pi_cap = 0;
-  bool fuse_net = true;      // network statistics fused into the profile kernel (NETREP_FUSE)
   double* d_scratch = nullptr;
   size_t scratch_cap = 0;
   int* d_counters = nullptr;  // [0] queue head, [1..4] lanczos diagnostics, [5] flag
@@ -301,18 +300,15 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   np.slot_cor_degree = data ? 3 : 2;
   np.slot_avg_cor = data ? 5 : 3;
   np.out = d_out;
-  // Default with data: the network statistics run inside the summary-profile
-  // kernel (fused per item), so their HBM-bound gathers overlap the matrix and
-  // Lanczos work of the co-resident workgroups. NETREP_FUSE=0 launches them
-  // as their own kernel (optionally on the side stream, NETREP_CONCURRENT=1).
+  // The network statistics are their own launch (module_net_kernel) ahead of
+  // the summary-profile kernel; NETREP_CONCURRENT=1 puts them on the side
+  // stream instead.
   ProfilePlan plan;
   if (data) {
     rc = plan_profile(ctx, n_items, ctx->k_max, (int)ctx->n_samples, &plan);
     if (rc) return rc;
   }
-  // Variant 4 keeps its matvec partials in global scratch; the network
-  // statistics (LDS weighted degrees) then run as their own kernel.
-  const bool fuse = data && ctx->fuse_net && plan.variant != 4;
+  const bool fuse = false;
   const bool fork = data && !fuse && ctx->concurrent;
   hipStream_t net_stream = fork ? ctx->side : ctx->stream;
   if (fork) {
@@ -528,7 +524,6 @@ int nr_ctx_create(int device, nr_ctx** out) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (const char* c = std::getenv("NETREP_CONCURRENT")) ctx->concurrent = std::atoi(c) != 0;
-  if (const char* f = std::getenv("NETREP_FUSE")) ctx->fuse_net = std::atoi(f) != 0;
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, 16 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, 16 * sizeof(int));

@@ -17,174 +17,282 @@
 
 #include "prp.h"
 #include "kernels.h"
+#include "device_common.h"
 
 namespace nr {
 
-#define NR_BS 256
-#define NR_WAVES (NR_BS / 64)
 
-__device__ __forceinline__ double nr_nan() { return __longlong_as_double(0x7FF8000000000000ll); }
+// ---------------------------------------------------------------------------
+// Weighted degree as the reference computes it (src/netStats.cpp:124-144):
+// the column sums of |net(srt, srt)| over the module's SORTED nodes with the
+// diagonal included, minus |diag|. arma::sum over a column is Armadillo's
+// arrayops::accumulate: two accumulators over the even and odd row
+// positions, returned as acc1 + acc2 (RcppArmadillo, unvendored; the same
+// loop is restated in oracle/netrep_ref.cpp). When |diag| dwarfs the
+// off-diagonal weights -- a correlation network's diagonal is 1 -- every
+// addition after the diagonal rounds to the accumulator's ulp, and those
+// roundings move cor.degree by up to ~1e-9 (measured on the
+// C5 shape). The kernel therefore reproduces them instead of summing exactly:
+//  * per node c (sorted position p, d = |diag|): the same-parity terms before
+//    p (Pb), the first same-parity term after p (F, from the node at position
+//    p + 2), the remaining same-parity terms (each rounded to the grid unit g
+//    of the accumulator once it holds the diagonal: added in units of g), and
+//    the other parity's sum (O);
+//  * Pb and O are accumulated in 64-bit fixed point (2^-16 g), the unit counts
+//    as integers, so the sums are exact and order independent (bitwise
+//    reproducible whatever the thread schedule);
+//  * WD = fl(fl(x + g * units + O) - d) with x = fl(fl(Pb + d) + F), valid
+//    while the accumulator stays in g's binade; otherwise (or d = 0) the plain
+//    sum of the off-diagonal terms, per-wave copies added in wave order.
+// Bitwise equal to the two-accumulator loop in the cancellation regime
+// (tools check: oracle/netrep_ref.cpp vs the kernel, tests/test_gpu_configs.py).
+// ---------------------------------------------------------------------------
+constexpr int WD_FX_BITS = 16;        // fixed-point sub-units per grid unit
+constexpr int WD_NO_GRID = -100000;   // exponent sentinel: no cancellation model
 
-// R's NA_real_ (src/permutations.cpp:383-384 fills non-finite with NA_REAL).
-__device__ __forceinline__ double na_fill(double x) {
-  return isfinite(x) ? x : __longlong_as_double(0x7FF00000000007A2ll);
+// Exponent of the grid unit g = 2^e of the accumulator holding d: the ulp of
+// d's binade, or of the next binade when d sits within 2^-20 below it (the
+// first addition then carries the accumulator across).
+__device__ __forceinline__ int wd_grid_exp(double d) {
+  if (!(d >= 2.2250738585072014e-308) || !isfinite(d)) return WD_NO_GRID;
+  const int e = ilogb(d);
+  const double top = ldexp(1.0, e + 1);
+  return (top - d <= ldexp(d, -20) ? e + 1 : e) - 52;
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+__device__ __forceinline__ unsigned long long wd_fx(double a, int ge, int extra) {
+  double v = ldexp(a, extra - ge);
+  v = v < 2.305843009213694e18 ? v : 2.305843009213694e18;  // 2^61: overflow is caught by the range check
+  return (unsigned long long)llrint(v);
 }
 
-// Block-wide sums of N values; result broadcast to every thread. `red` must
-// hold N * NR_WAVES doubles of LDS. Contains two barriers.
-template <int N, int NW = NR_WAVES>
-__device__ __forceinline__ void block_sums(double (&v)[N], double* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) red[i * NW + wave] = v[i];
+struct NetLds {
+  double* red;                       // 8 * NW
+  uint32_t* idx;                     // [k] test column of each node
+  int* rk;                           // [k] sorted position (SortNodes rank)
+  int* ge;                           // [k] grid exponent (WD_NO_GRID: none)
+  double* dg;                        // [k] |diag|
+  double* plain;                     // [NW][k] plain off-diagonal sums, per wave
+  unsigned long long *pb, *on, *tn;  // [k] fixed-point Pb, O; unit count of the rest
+  double* ff;                        // [k] the first same-parity term after the diagonal
+  int k_stride;
+};
+
+template <int NW>
+__device__ __forceinline__ NetLds carve_net_lds(unsigned char* smem, int kmax) {
+  NetLds L;
+  L.red = reinterpret_cast<double*>(smem);
+  L.plain = L.red + 8 * NW;
+  L.dg = L.plain + (size_t)NW * kmax;
+  L.ff = L.dg + kmax;
+  L.pb = reinterpret_cast<unsigned long long*>(L.ff + kmax);
+  L.on = L.pb + kmax;
+  L.tn = L.on + kmax;
+  L.idx = reinterpret_cast<uint32_t*>(L.tn + kmax);
+  L.rk = reinterpret_cast<int*>(L.idx + kmax);
+  L.ge = L.rk + kmax;
+  L.k_stride = kmax;
+  return L;
+}
+
+size_t net_lds_bytes(int nw, int kmax) {
+  return sizeof(double) * (8 * (size_t)nw + (size_t)(nw + 2) * kmax) + sizeof(unsigned long long) * 3 * (size_t)kmax +
+         sizeof(int) * 3 * (size_t)kmax;
+}
+
+// One weighted-degree contribution a = |net(source, target)| (a >= 0).
+__device__ __forceinline__ void wd_add(const NetLds& L, double* plain_w, int t, int pt, int ps, double a) {
+  atomicAdd(&plain_w[t], a);
+  const int ge = L.ge[t];
+  if (ge == WD_NO_GRID || !isfinite(a)) return;
+  if (((pt ^ ps) & 1) == 0) {
+    if (ps < pt) atomicAdd(&L.pb[t], wd_fx(a, ge, WD_FX_BITS));
+    else if (ps == pt + 2) atomicAdd(&L.ff[t], a);
+    else atomicAdd(&L.tn[t], wd_fx(a, ge, 0));
+  } else {
+    atomicAdd(&L.on[t], wd_fx(a, ge, WD_FX_BITS));
   }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[i * NW + w];
-    v[i] = s;
-  }
-  __syncthreads();
 }
 
-// Pearson correlation from (shifted) one-pass sums over complete cases.
-__device__ __forceinline__ double pearson_sums(double n, double sx, double sy,
-                                               double sxx, double syy, double sxy) {
-  if (n < 1.0) return nr_nan();
-  const double cov = sxy - sx * sy / n;
-  const double vx = sxx - sx * sx / n;
-  const double vy = syy - sy * sy / n;
-  return cov / (sqrt(vx) * sqrt(vy));
-}
-
-// Test column of module node c of item (p, m): GetRandomIdx
-// (src/utils.cpp:193-199) under a PRP, an explicit table, or a direct set.
-__device__ __forceinline__ uint32_t node_index(const IndexSource& src, const nr_prp_key& key,
-                                               int64_t p_local, int64_t node) {
-  if (src.mode == NR_IDX_DIRECT) return (uint32_t)src.direct_idx[node];
-  const uint32_t q = (uint32_t)src.null_pos[node];
-  const uint32_t s = (src.mode == NR_IDX_PRP)
-                         ? nr_prp_permute(key, q)
-                         : src.pi[p_local * (int64_t)src.n_null + q];
-  return (uint32_t)src.null_idx[s];
-}
-
-// Decode flat CorrVector position v -> (jj, ii), ii > jj, column-major lower
-// triangle (src/netStats.cpp:196-201).
-__device__ __forceinline__ void decode_pair(int64_t v, int64_t k, int64_t& jj, int64_t& ii) {
-  const double b = (double)(2 * k - 1);
-  int64_t j = (int64_t)floor((b - sqrt(b * b - 8.0 * (double)v)) * 0.5);
-  if (j < 0) j = 0;
-  // off(j) = j*(2k-j-1)/2 pairs precede column j
-  while (j > 0 && j * (2 * k - j - 1) / 2 > v) --j;
-  while ((j + 1) * (2 * k - j - 2) / 2 <= v) ++j;
-  jj = j;
-  ii = v - j * (2 * k - j - 1) / 2 + j + 1;
+// The reference's weighted degree of node c from its accumulated parts.
+__device__ __forceinline__ double wd_final(const NetLds& L, int NWn, int c, int k) {
+  double plain = 0.0;
+  for (int w = 0; w < NWn; ++w) plain += L.plain[w * L.k_stride + c];
+  const double d = L.dg[c];
+  if (!isfinite(d)) return nr_nan();      // colsum carries the NaN/Inf diagonal, minus itself
+  if (!isfinite(plain)) return plain;
+  const int ge = L.ge[c];
+  if (ge == WD_NO_GRID) return plain;
+  // fixed point valid (no 2^61 clamp reached) and the sums small against d
+  if (ldexp(plain, WD_FX_BITS - ge) >= 1.1529215046068470e18) return plain;  // 2^60
+  const double s = ldexp(1.0, ge - WD_FX_BITS);
+  const double g = ldexp(1.0, ge);
+  const double pb = (double)L.pb[c] * s;
+  const double o = (double)L.on[c] * s;
+  double x = pb + d;
+  if (L.rk[c] + 2 < k) x = x + L.ff[c];
+  if (!(x > 0.0) || ilogb(x) - 52 != ge) return plain;   // the predicted grid was not x's
+  const double chain = x + (double)L.tn[c] * g;
+  if (ilogb(chain) - 52 != ge) return plain;              // the accumulator left g's binade
+  return (chain + o) - d;
 }
 
 // ---------------------------------------------------------------------------
 // Module network statistics of one item (p, m): avg.weight, cor.cor,
 // cor.degree, avg.cor (CorrVector + WeightedDegree gathers, src/netStats.cpp:
-// 124-204; src/permutations.cpp:75-97). Run by a whole NW-wave workgroup,
-// either as its own kernel (one workgroup per item) or fused into the
-// summary-profile bodies, where its HBM-bound gather overlaps the matrix /
-// latency-bound work of the co-resident workgroups. idx[0..k) (LDS) holds the
-// item's test columns; wd is NW x wd_stride doubles of LDS scratch; red holds
-// 8 * NW doubles.
+// 124-204; src/permutations.cpp:75-97). One NW-wave workgroup per item. The
+// k(k-1)/2 pairs (column-major lower triangle of the unsorted module order,
+// CorrVector's order) are cut into chunks of CH consecutive pairs dealt
+// round-robin to the threads; a thread walks its chunk with U random 16-byte
+// gathers in flight, keeps the column's (target jj) weighted-degree parts in
+// registers and flushes them at a column change, and adds the row node's
+// (target ii) parts in LDS, where the targets of one wave instruction are
+// distinct (no same-address atomics). L.idx holds the item's test columns.
 // ---------------------------------------------------------------------------
-template <int NW, int U = 8>
+template <int NW, int U = 8, int CH = 8>
 __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_local, int64_t off, int64_t k,
-                                         const uint32_t* idx, double* red, double* wd, int wd_stride) {
+                                         const NetLds& L) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x;
-  // Each wave accumulates the weighted degrees into its own copy: the pair ->
-  // (wave, lane, iteration) assignment is fixed, so the sums are bitwise
-  // reproducible; the copies are added in wave order afterwards.
-  double* wdw = wd + (threadIdx.x >> 6) * wd_stride;
+  const int wave = tid >> 6;
+  const double2* __restrict__ pairs = P.pairs;
+  const int64_t n = P.n_nodes;
+  // per node: sorted position (SortNodes, src/netStats.cpp:23-32), |diag|,
+  // grid exponent, zeroed accumulators
   for (int64_t c = tid; c < k; c += BS) {
+    const uint32_t ic = L.idx[c];
+    int r = 0;
+    for (int64_t c2 = 0; c2 < k; ++c2) r += L.idx[c2] < ic;
+    L.rk[c] = r;
+    const double d = fabs(pairs[(int64_t)ic + (int64_t)ic * n].y);
+    L.dg[c] = d;
+    L.ge[c] = wd_grid_exp(d);
 #pragma unroll
-    for (int w = 0; w < NW; ++w) wd[w * wd_stride + c] = 0.0;
+    for (int w = 0; w < NW; ++w) L.plain[w * L.k_stride + c] = 0.0;
+    L.pb[c] = 0;
+    L.on[c] = 0;
+    L.tn[c] = 0;
+    L.ff[c] = 0.0;
   }
   __syncthreads();
 
   const int64_t npairs = k * (k - 1) / 2;
   const int64_t cvo = P.cv_off[m];
-  const double2* __restrict__ pairs = P.pairs;
-  const int64_t n = P.n_nodes;
+  double* plain_w = L.plain + wave * L.k_stride;
   // Shifts keep the one-pass sums well conditioned and make a constant
   // vector give exactly zero variance, as the reference's two-pass stddev does.
   // The test-side shift is the item's first pair; a non-finite first pair
   // (dropped by CompleteCases, src/netStats.cpp:43-61) falls back to 0 so it
   // cannot poison the other pairs' sums.
   const double xs = P.cv_shift ? P.cv_shift[m] : 0.0;
-  const double y0 = npairs > 0 ? pairs[(int64_t)idx[1] + (int64_t)idx[0] * n].x : 0.0;
+  const double y0 = npairs > 0 ? pairs[(int64_t)L.idx[1] + (int64_t)L.idx[0] * n].x : 0.0;
   const double ys = isfinite(y0) ? y0 : 0.0;
 
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // n, sx, sy, sxx, syy, sxy, s(sign(x) y)
-  // U: pairs in flight per thread (random 16-byte gathers)
-  for (int64_t v0 = tid; v0 < npairs; v0 += (int64_t)BS * U) {
-    double2 e[U];
-    double e2[U];
-    double x[U];
-    int jjs[U], iis[U];
+  const int64_t nchunks = (npairs + CH - 1) / CH;
+  for (int64_t ch = tid; ch < nchunks; ch += BS) {
+    const int64_t v0 = ch * CH;
+    const int64_t v1 = v0 + CH < npairs ? v0 + CH : npairs;
+    int64_t jj64, ii64;
+    decode_pair(v0, k, jj64, ii64);
+    int jj = (int)jj64, ii = (int)ii64;
+    // the column's parts, in registers until the column changes
+    int pj = L.rk[jj];
+    int gj = L.ge[jj];
+    double cpl = 0.0, cff = 0.0;
+    unsigned long long cpb = 0, con = 0, ctn = 0;
+    for (int64_t vb = v0; vb < v1; vb += U) {
+      double2 e[U];
+      double e2[U];
+      double x[U];
+      int iis[U], jjs[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t v = v0 + (int64_t)u * BS;
-      jjs[u] = -1;
-      iis[u] = 0;
-      e[u] = make_double2(0.0, 0.0);
-      e2[u] = 0.0;
-      x[u] = 0.0;
-      if (v < npairs) {
-        int64_t jj, ii;
-        decode_pair(v, k, jj, ii);
-        jjs[u] = (int)jj;
-        iis[u] = (int)ii;
-        const int64_t r = idx[ii], c = idx[jj];
-        e[u] = pairs[r + c * n];                      // corr(idx[ii], idx[jj]), net(idx[ii], idx[jj])
-        e2[u] = P.symmetric ? e[u].y : pairs[c + r * n].y;  // net(idx[jj], idx[ii])
-        x[u] = P.disc_cv ? P.disc_cv[cvo + v] : nr_nan();
+      for (int u = 0; u < U; ++u) {
+        const int64_t v = vb + u;
+        iis[u] = -1;
+        jjs[u] = jj;
+        e[u] = make_double2(0.0, 0.0);
+        e2[u] = 0.0;
+        x[u] = 0.0;
+        if (v < v1) {
+          iis[u] = ii;
+          const int64_t r = L.idx[ii], c = L.idx[jj];
+          e[u] = pairs[r + c * n];                              // corr(idx[ii], idx[jj]), net(idx[ii], idx[jj])
+          e2[u] = P.symmetric ? e[u].y : pairs[c + r * n].y;    // net(idx[jj], idx[ii])
+          x[u] = P.disc_cv ? P.disc_cv[cvo + v] : nr_nan();
+          if (++ii == k) {
+            ++jj;
+            ii = jj + 1;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (iis[u] >= 0) {
+          const int i = iis[u], j = jjs[u];
+          if (j != jj64) {  // the chunk crossed into column j: flush the previous column
+            const int jp = (int)jj64;
+            atomicAdd(&plain_w[jp], cpl);
+            if (gj != WD_NO_GRID) {
+              atomicAdd(&L.pb[jp], cpb);
+              atomicAdd(&L.on[jp], con);
+              atomicAdd(&L.tn[jp], ctn);
+              atomicAdd(&L.ff[jp], cff);
+            }
+            cpl = cff = 0.0;
+            cpb = con = ctn = 0;
+            jj64 = j;
+            pj = L.rk[j];
+            gj = L.ge[j];
+          }
+          const double y = e[u].x;
+          if (P.cv_out) P.cv_out[cvo + vb + u] = y;
+          const int pi = L.rk[i];
+          // target jj (column idx[jj]) gains row idx[ii]: registers
+          const double a = fabs(e[u].y);
+          cpl += a;
+          if (gj != WD_NO_GRID && isfinite(a)) {
+            if (((pj ^ pi) & 1) == 0) {
+              if (pi < pj) cpb += wd_fx(a, gj, WD_FX_BITS);
+              else if (pi == pj + 2) cff += a;
+              else ctn += wd_fx(a, gj, 0);
+            } else {
+              con += wd_fx(a, gj, WD_FX_BITS);
+            }
+          }
+          // target ii (column idx[ii]) gains row idx[jj]: LDS
+          wd_add(L, plain_w, i, pi, pj, fabs(e2[u]));
+          const double xv = x[u];
+          if (isfinite(xv) && isfinite(y)) {        // CompleteCases src/netStats.cpp:43-61
+            const double dx = xv - xs, dy = y - ys;
+            acc[0] += 1.0;
+            acc[1] += dx;
+            acc[2] += dy;
+            acc[3] += dx * dx;
+            acc[4] += dy * dy;
+            acc[5] += dx * dy;
+            acc[6] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
+          }
+        }
       }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (jjs[u] >= 0) {
-      const double y = e[u].x;
-      if (P.cv_out) P.cv_out[cvo + v0 + (int64_t)u * BS] = y;
-      atomicAdd(&wdw[jjs[u]], fabs(e[u].y));    // column idx[jj] gains row idx[ii]
-      atomicAdd(&wdw[iis[u]], fabs(e2[u]));     // column idx[ii] gains row idx[jj]
-      const double xv = x[u];
-      if (isfinite(xv) && isfinite(y)) {        // CompleteCases src/netStats.cpp:43-61
-        const double dx = xv - xs, dy = y - ys;
-        acc[0] += 1.0;
-        acc[1] += dx;
-        acc[2] += dy;
-        acc[3] += dx * dx;
-        acc[4] += dy * dy;
-        acc[5] += dx * dy;
-        acc[6] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
-      }
+    {  // flush the last column of the chunk
+      const int jp = (int)jj64;
+      atomicAdd(&plain_w[jp], cpl);
+      if (gj != WD_NO_GRID) {
+        atomicAdd(&L.pb[jp], cpb);
+        atomicAdd(&L.on[jp], con);
+        atomicAdd(&L.tn[jp], ctn);
+        atomicAdd(&L.ff[jp], cff);
       }
     }
   }
-  block_sums<7, NW>(acc, red);
-  for (int64_t c = tid; c < k; c += BS) {
-    double s = wd[c];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) s += wd[w * wd_stride + c];
-    wd[c] = s;
-  }
+  block_sums<7, NW>(acc, L.red);   // its barriers also complete the weighted-degree parts
+
+  // Weighted degrees (the reference's rounding, wd_final), into plain[0]:
+  // node c's parts are read and overwritten by its owner thread only
+  double* wd = L.plain;
+  for (int64_t c = tid; c < k; c += BS) wd[c] = wd_final(L, NW, (int)c, (int)k);
   __syncthreads();
 
   // Weighted degree statistics: two-pass over the k values held in LDS.
@@ -200,7 +308,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
       a1[3] += y;
     }
   }
-  block_sums<4, NW>(a1, red);
+  block_sums<4, NW>(a1, L.red);
   const double mx = a1[2] / a1[1], my = a1[3] / a1[1];
   double a2[3] = {0, 0, 0};
   for (int64_t c = tid; c < k; c += BS) {
@@ -214,7 +322,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     }
     if (P.wd_out) P.wd_out[woff + c] = y;
   }
-  block_sums<3, NW>(a2, red);
+  block_sums<3, NW>(a2, L.red);
 
   // AverageEdgeWeight src/netStats.cpp:154-162: unsigned int pair count.
   const uint32_t ku = (uint32_t)k;
@@ -230,16 +338,16 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     o[(int64_t)P.n_rows * P.slot_cor_degree] = na_fill(cor_degree);
     o[(int64_t)P.n_rows * P.slot_avg_cor] = na_fill(avg_cor);
   }
-  __syncthreads();  // wd / red free again
+  __syncthreads();  // LDS free again
 }
 
-// Kernel 1: module network statistics. One workgroup per item.
-__global__ void __launch_bounds__(NR_BS)
+// Kernel 1: module network statistics. One workgroup of NW waves per item
+// (NW = 2 for modules too large for four waves' LDS copies).
+template <int NW>
+__global__ void __launch_bounds__(NW * 64)
 module_net_kernel(NetParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* red = reinterpret_cast<double*>(smem);                    // 8 * NR_WAVES
-  double* wd = red + 8 * NR_WAVES;                                  // [NR_WAVES][k_max]
-  uint32_t* idx = reinterpret_cast<uint32_t*>(wd + NR_WAVES * P.k_max);  // [k]
+  const NetLds L = carve_net_lds<NW>(smem, P.k_max);
   const int64_t item = blockIdx.x;
   const int64_t mslot = item / P.n_perm;
   const int64_t p_local = item - mslot * P.n_perm;
@@ -248,176 +356,11 @@ module_net_kernel(NetParams P) {
   const int64_t k = P.node_off[m + 1] - off;
   nr_prp_key key;
   if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
-  for (int64_t c = threadIdx.x; c < k; c += NR_BS) idx[c] = node_index(P.src, key, p_local, off + c);
+  for (int64_t c = threadIdx.x; c < k; c += NW * 64) L.idx[c] = node_index(P.src, key, p_local, off + c);
   __syncthreads();
-  net_item<NR_WAVES>(P, m, p_local, off, k, idx, red, wd, P.k_max);
+  net_item<NW>(P, m, p_local, off, k, L);
 }
 
-// ---------------------------------------------------------------------------
-// Kernel 2: summary-profile statistics. Persistent workgroups pull items from
-// a queue; each owns a scratch slot holding G = X^T X and the Lanczos basis.
-// ---------------------------------------------------------------------------
-typedef double nr_f64x4 __attribute__((ext_vector_type(4)));
-
-// 1/d: v_rcp_f64 refined by two Newton steps as in the compiler's own
-// division expansion, without its scaling/fixup (d normal, |d| >= 1e-300);
-// used only in the Sturm counts of the Ritz checks.
-__device__ __forceinline__ double nr_rcp(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  r = fma(r, fma(-d, r, 1.0), r);
-  r = fma(r, fma(-d, r, 1.0), r);
-  return r;
-}
-
-// Largest eigenvalue of the symmetric tridiagonal (alpha[0..n), beta[0..n-1))
-// by 64-way multisection on Sturm counts; executed by one full wave. The
-// counts use the characteristic-polynomial recurrence of the Gershgorin-
-// normalised matrix, p_i = (a_i - x) p_{i-1} - b_{i-1}^2 p_{i-2} (sign changes
-// of p_0..p_n = eigenvalues below x): one FMA on the dependency chain per
-// step and no division; |p| is renormalised every 4 steps.
-__device__ double tri_top_eigenvalue(const double* alpha, const double* beta, int n, int lane) {
-  double lo = alpha[0], hi = alpha[0];
-  for (int i = lane; i < n; i += 64) {
-    const double r = (i > 0 ? fabs(beta[i - 1]) : 0.0) + (i < n - 1 ? fabs(beta[i]) : 0.0);
-    lo = fmin(lo, alpha[i] - r);
-    hi = fmax(hi, alpha[i] + r);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
-  }
-  const double scale = fmax(fabs(lo), fabs(hi)) + 1e-300;
-  const double inv = 1.0 / scale;
-  lo -= 1e-14 * scale;
-  hi += 1e-14 * scale;
-  for (int it = 0; it < 12; ++it) {
-    const double x = (lo + (hi - lo) * (double)(lane + 1) / 65.0) * inv;
-    double p0 = 1.0, p1 = alpha[0] * inv - x;
-    int cnt = p1 < 0.0;  // eigenvalues < x
-#pragma unroll 4
-    for (int i = 1; i < n; ++i) {
-      const double b = beta[i - 1] * inv;
-      const double p2 = fma(alpha[i] * inv - x, p1, -(b * b) * p0);
-      cnt += (p2 < 0.0) != (p1 < 0.0);
-      p0 = p1;
-      p1 = p2;
-      if ((i & 3) == 0) {
-        const double mg = fabs(p1);
-        const double s = mg > 1e150 ? 1e-150 : (mg < 1e-150 ? 1e150 : 1.0);
-        p0 *= s;
-        p1 *= s;
-      }
-    }
-    // largest x with cnt <= n-1 becomes lo; smallest x with cnt == n becomes hi
-    const unsigned long long below = __ballot(cnt <= n - 1);
-    // lanes are ordered by x: lanes [0, t) have cnt <= n-1, lanes [t, 64) have cnt == n
-    const int t = __popcll(below);
-    const double xlo = lo + (hi - lo) * (double)t / 65.0;
-    const double xhi = lo + (hi - lo) * (double)(t + 1) / 65.0;
-    lo = xlo;
-    hi = xhi;
-    if (hi - lo <= 2e-16 * scale) break;
-  }
-  return 0.5 * (lo + hi);
-}
-
-// Convergence estimate of the top Ritz pair: |last component| of the unit
-// eigenvector y of the tridiagonal for theta, times beta_j. y comes from the
-// three-term recurrence run BACKWARDS from y_{n-1} = 1: the top eigenvector
-// of an unreduced Jacobi matrix is positive and its tail decays once the
-// pair converges, so upward it is the dominant (stable) solution. rb holds
-// 1/beta[0..n-1), one wave fills it. Returns beta_j / |y| (lane 0).
-__device__ double tri_top_resid(const double* alpha, const double* beta, int n, double theta, double beta_j,
-                                double* rb, int lane) {
-  for (int i = lane; i < n - 1; i += 64) rb[i] = 1.0 / beta[i];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  double y1 = 1.0, y2 = 0.0, ss = 1.0;  // y_i, y_{i+1}, sum of squares
-  for (int i = n - 1; i > 0; --i) {
-    const double y0 = fma(theta - alpha[i], y1, -(i < n - 1 ? beta[i] : 0.0) * y2) * rb[i - 1];
-    ss = fma(y0, y0, ss);
-    y2 = y1;
-    y1 = y0;
-    if (ss > 1e200) {
-      y1 *= 1e-100;
-      y2 *= 1e-100;
-      ss *= 1e-200;
-      beta_j *= 1e-100;
-    }
-  }
-  return beta_j / sqrt(ss);
-}
-
-// Eigenvector of the tridiagonal for eigenvalue theta by two steps of inverse
-// iteration; LU with partial pivoting as LAPACK dgttrf/dgtts2. Single lane.
-// y[0..n) comes back normalised; work holds 5n doubles.
-__device__ void tri_eigenvector(const double* alpha, const double* beta, int n, double theta,
-                                double* y, double* work) {
-  double* dl = work;
-  double* d = work + n;
-  double* du = work + 2 * n;
-  double* du2 = work + 3 * n;
-  double* swp = work + 4 * n;
-  double scale = fabs(theta);
-  for (int i = 0; i < n; ++i) {
-    d[i] = alpha[i] - theta;
-    scale = fmax(scale, fabs(alpha[i]));
-    if (i < n - 1) {
-      du[i] = beta[i];
-      dl[i] = beta[i];
-      scale = fmax(scale, fabs(beta[i]));
-    }
-    du2[i] = 0.0;
-    swp[i] = 0.0;
-  }
-  const double floor_piv = 1e-300 + 2.2e-16 * scale;
-  for (int i = 0; i < n - 1; ++i) {
-    if (fabs(d[i]) >= fabs(dl[i])) {
-      if (fabs(d[i]) < floor_piv) d[i] = d[i] < 0.0 ? -floor_piv : floor_piv;
-      const double f = dl[i] / d[i];
-      dl[i] = f;
-      d[i + 1] -= f * du[i];
-    } else {
-      const double f = d[i] / dl[i];
-      d[i] = dl[i];
-      dl[i] = f;
-      const double t = du[i];
-      du[i] = d[i + 1];
-      d[i + 1] = t - f * d[i + 1];
-      if (i < n - 2) {
-        du2[i] = du[i + 1];
-        du[i + 1] = -f * du[i + 1];
-      }
-      swp[i] = 1.0;
-    }
-  }
-  if (fabs(d[n - 1]) < floor_piv) d[n - 1] = d[n - 1] < 0.0 ? -floor_piv : floor_piv;
-  for (int i = 0; i < n; ++i) y[i] = 1.0;
-  for (int iter = 0; iter < 2; ++iter) {
-    for (int i = 0; i < n - 1; ++i) {
-      if (swp[i] == 0.0) {
-        y[i + 1] -= dl[i] * y[i];
-      } else {
-        const double t = y[i];
-        y[i] = y[i + 1];
-        y[i + 1] = t - dl[i] * y[i];
-      }
-    }
-    y[n - 1] /= d[n - 1];
-    if (n > 1) y[n - 2] = (y[n - 2] - du[n - 2] * y[n - 1]) / d[n - 2];
-    for (int i = n - 3; i >= 0; --i) y[i] = (y[i] - du[i] * y[i + 1] - du2[i] * y[i + 2]) / d[i];
-    double mx = 0.0;
-    for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(y[i]));
-    double nrm = 0.0;
-    for (int i = 0; i < n; ++i) {
-      y[i] /= mx;
-      nrm += y[i] * y[i];
-    }
-    const double inv = 1.0 / sqrt(nrm);
-    for (int i = 0; i < n; ++i) y[i] *= inv;
-  }
-}
 
 // w = G x over the leading k x k block of G (column-major, leading dimension
 // ld, symmetric, both triangles stored). Waves take contiguous column ranges,
@@ -539,33 +482,6 @@ __device__ __forceinline__ double reorthogonalise_cgs(const double* __restrict__
   return nrm[0];
 }
 
-// Partial reorthogonalisation (Simon 1984): omega_{j+1,i} estimates q_{j+1}.q_i
-// from the recurrence on T's entries; run by one wave over i = 0..j. Returns
-// max_i |omega_{j+1,i}| (all lanes). om_cur = omega_{j,.}, om_prev = omega_{j-1,.}.
-__device__ __forceinline__ double omega_update(const double* alpha, const double* beta, int j, double beta_j,
-                                               const double* om_cur, const double* om_prev, double* om_next,
-                                               double anorm, int k, int lane) {
-  const double eps = 2.220446049250313e-16;
-  const double psi = eps * anorm / beta_j;
-  double mx = 0.0;
-  for (int i = lane; i < j; i += 64) {
-    double t = beta[i] * om_cur[i + 1] + (alpha[i] - alpha[j]) * om_cur[i] -
-               (j > 0 ? beta[j - 1] * om_prev[i] : 0.0);
-    if (i > 0) t += beta[i - 1] * om_cur[i - 1];
-    t = t / beta_j;
-    t += t >= 0.0 ? psi : -psi;
-    om_next[i] = t;
-    mx = fmax(mx, fabs(t));
-  }
-  if (lane == 0) {
-    om_next[j] = eps * sqrt((double)k) * anorm / beta_j;
-    om_next[j + 1] = 1.0;
-    mx = fmax(mx, fabs(om_next[j]));
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-  return mx;
-}
 
 // Packed symmetric storage: lower triangle, column-major, over kc = k + 1
 // columns (the last is the virtual all-ones column); column c holds rows
@@ -684,52 +600,6 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
   }
 }
 
-// Cross-lane butterfly steps without LDS (gfx950): v_permlane32_swap /
-// v_permlane16_swap exchange half-waves / odd-even rows of two registers, so
-// x' + y' leaves lanes [0,32) with x summed over the lane pair (l, l^32) and
-// lanes [32,64) with y summed likewise (16-lane rows for the 16 variant).
-__device__ __forceinline__ double nr_swap32_sum(double x, double y) {
-  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(y), false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(y), false, false);
-  return __hiloint2double((int)hi[0], (int)lo[0]) + __hiloint2double((int)hi[1], (int)lo[1]);
-}
-__device__ __forceinline__ double nr_swap16_sum(double x, double y) {
-  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(y), false, false);
-  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(y), false, false);
-  return __hiloint2double((int)hi[0], (int)lo[0]) + __hiloint2double((int)hi[1], (int)lo[1]);
-}
-// DPP lane moves within 16-lane rows (both dwords of a double).
-template <int CTRL>
-__device__ __forceinline__ double nr_dpp(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-constexpr int NR_DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
-constexpr int NR_DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
-constexpr int NR_DPP_ROR8 = 0x128;        // row_ror:8 == lane ^ 8 within a row
-constexpr int NR_DPP_HALF_MIRROR = 0x141; // lane ^ 7 within 8 lanes (flips bit 2)
-
-// Transpose-reduce of 16 per-lane column partials up[0..16) over the 64 rows
-// (lanes) of a unit: afterwards lanes with (lane & 3) == 0 hold the column
-// sum of column 8*b5 + 4*b4 + 2*b3 + b2 (b = lane bits). 8 + 4 swaps, 3 + 2
-// DPP-exchange levels; no LDS traffic.
-__device__ __forceinline__ double nr_transpose_reduce16(const double (&up)[16], int lane) {
-  double a8[8], a4[4], a2[2];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) a8[i] = nr_swap32_sum(up[i], up[i + 8]);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) a4[i] = nr_swap16_sum(a8[i], a8[i + 4]);
-  const bool b3 = lane & 8;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-    a2[i] = (b3 ? a4[i + 2] : a4[i]) + nr_dpp<NR_DPP_ROR8>(b3 ? a4[i] : a4[i + 2]);
-  const bool b2 = lane & 4;
-  double v = (b2 ? a2[1] : a2[0]) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? a2[0] : a2[1]);
-  v += nr_dpp<NR_DPP_XOR2>(v);
-  v += nr_dpp<NR_DPP_XOR1>(v);
-  return v;
-}
 
 // w = G x over the leading k x k block of the PACKED symmetric G (pk_at), NW
 // waves. Work units are (64-row block, 16-column group) pairs with columns
@@ -877,52 +747,8 @@ __device__ __forceinline__ double reorthogonalise_bf(const double* __restrict__ 
 //   node contributions (profile_contrib) -> statistics (profile_stats).
 // ---------------------------------------------------------------------------
 
-// LDS carve-out common to all summary-profile bodies.
-struct LzLds {
-  double *red, *q, *qprev, *w, *vv, *gv, *colm;
-  double *alpha, *beta, *h, *ty, *twork, *omg;
-  uint32_t* idx;
-  int mmax;
-};
 
-// Carves red, q, qprev, w, vv, gv, colm (kvec each), then `extra` doubles for
-// the storage scheme (returned in *extra_out), then the Lanczos tridiagonal
-// arrays and idx. Layout matches profile_kernel_lds / reg_kernel_lds.
-template <int NW>
-__device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mmax, int64_t extra,
-                                           double** extra_out) {
-  LzLds L;
-  L.red = reinterpret_cast<double*>(smem);  // 8 * NW
-  L.q = L.red + 8 * NW;
-  L.qprev = L.q + kvec;
-  L.w = L.qprev + kvec;
-  L.vv = L.w + kvec;
-  L.gv = L.vv + kvec;
-  L.colm = L.gv + kvec;
-  *extra_out = L.colm + kvec;
-  L.alpha = *extra_out + extra;  // [mmax]
-  L.beta = L.alpha + mmax;       // [mmax]
-  L.h = L.beta + mmax;           // [mmax]
-  L.ty = L.h + mmax;             // [mmax]
-  L.twork = L.ty + mmax;         // [5 * mmax]
-  L.omg = L.twork + 5 * mmax;    // [3 * (mmax + 1)] omega rows
-  L.idx = reinterpret_cast<uint32_t*>(L.omg + 3 * (mmax + 1));  // [kvec]
-  L.mmax = mmax;
-  return L;
-}
 
-// Phase stamps (diagnostics only: active when P.stamps != NULL, a separate
-// measurement run; no stamp executes otherwise). Thread 0 accumulates shader
-// cycles per phase between the barriers that already delimit the phases.
-__device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memtime(); }
-#define NR_STAMP(slot)                                                          \
-  do {                                                                          \
-    if (P.stamps && threadIdx.x == 0) {                                         \
-      const uint64_t t_ = nr_clock();                                           \
-      atomicAdd((unsigned long long*)&P.stamps[slot], (unsigned long long)(t_ - t_mark)); \
-      t_mark = t_;                                                              \
-    }                                                                           \
-  } while (0)
 
 // Lanczos for the top eigenpair of the k x k operator mv (mv(x, out, y)
 // writes out = G x for rows < k and returns y . out; x is zero beyond k):
@@ -1075,145 +901,9 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   __syncthreads();
 }
 
-// Node contributions from the Ritz vector (u = X v / sigma):
-//   NC_j = cor(x_j, u) = ((Gv)_j/sigma - S m_j ubar) / sqrt((G_jj - S m_j^2)(1 - S ubar^2)),
-// oriented by sign(cor(rowMeans(X), u)) (src/netStats.cpp:242-247, 279); the
-// result goes to L.w. diag(c) = G_cc; L.colm holds the column means.
-template <int NW, class MV, class DG>
-__device__ __forceinline__ void profile_contrib(const ProfileParams& P, int k, int m, const LzLds& L,
-                                                const double* __restrict__ X, int S, double ones_g_ones,
-                                                MV& mv, DG diag) {
-  constexpr int BS = NW * 64;
-  const int tid = threadIdx.x;
-  const double Sd = (double)S;
-  double* vv = L.vv;
-  double* gv = L.gv;
-  double* colm = L.colm;
-  mv(vv, gv, nullptr);
-  // lambda = v.Gv; ubar = mean of u = X v / sigma
-  double a3[2] = {0.0, 0.0};
-  for (int c = tid; c < k; c += BS) {
-    a3[0] += vv[c] * gv[c];
-    a3[1] += colm[c] * vv[c];
-  }
-  block_sums<2, NW>(a3, L.red);
-  const double lambda = a3[0];
-  const double sigma = sqrt(lambda);
-  const double ubar = a3[1] / sigma;
-  const double var_u = 1.0 - Sd * ubar * ubar;  // sum (u - ubar)^2 with |u| = 1
-  // orientation: sign(cor(meanObs, u)) (src/netStats.cpp:242-247); the sign
-  // of the covariance is that of sum_j cov(x_j, u); var(meanObs) * k^2 * (S-1)
-  // = 1'G1 - (sum of all data)^2 / S.
-  double a4[2] = {0.0, 0.0};
-  for (int c = tid; c < k; c += BS) {
-    a4[0] += gv[c] / sigma - Sd * colm[c] * ubar;
-    a4[1] += colm[c];
-  }
-  block_sums<2, NW>(a4, L.red);
-  const double var_mo = ones_g_ones - Sd * a4[1] * a4[1];
-  const bool flip = (a4[0] < 0.0) && (var_mo > 0.0) && (var_u > 0.0);
-  const double sgn = flip ? -1.0 : 1.0;
-  // NC_j = cor(x_j, u) (src/netStats.cpp:279); node order = CSR order
-  for (int c = tid; c < k; c += BS) {
-    const double cov = gv[c] / sigma - Sd * colm[c] * ubar;
-    const double var_x = diag(c) - Sd * colm[c] * colm[c];
-    L.w[c] = sgn * cov / (sqrt(var_x) * sqrt(var_u));
-  }
-  if (P.sp_out) {
-    for (int r = tid; r < S; r += BS) {
-      double s = 0.0;
-      for (int c = 0; c < k; ++c) s += X[(int64_t)L.idx[c] * S + r] * vv[c];
-      P.sp_out[(int64_t)m * S + r] = sgn * s / sigma;
-    }
-  }
-  __syncthreads();
-}
 
-// svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235).
-template <int NW>
-__device__ __forceinline__ void profile_nonfinite(const ProfileParams& P, int k, int m, int S, const LzLds& L) {
-  constexpr int BS = NW * 64;
-  for (int c = threadIdx.x; c < k; c += BS) L.w[c] = nr_nan();
-  if (P.sp_out)
-    for (int r = threadIdx.x; r < S; r += BS) P.sp_out[(int64_t)m * S + r] = nr_nan();
-  __syncthreads();
-}
 
-// ModuleCoherence (src/netStats.cpp:293-305), Correlation / SignAwareMean
-// against the discovery contribution (src/permutations.cpp:99,101); node
-// contributions in L.w.
-template <int NW>
-__device__ __forceinline__ void profile_stats(const ProfileParams& P, int k, int m, int64_t off,
-                                              int64_t p_local, const LzLds& L) {
-  constexpr int BS = NW * 64;
-  const int tid = threadIdx.x;
-  const double* w = L.w;
-  double b1[5] = {0, 0, 0, 0, 0};  // nfinite, sum nc^2, ncc, sx, sy
-  for (int c = tid; c < k; c += BS) {
-    const double y = w[c];
-    if (isfinite(y)) { b1[0] += 1.0; b1[1] += y * y; }
-    if (P.disc_nc) {
-      const double xv = P.disc_nc[off + c];
-      if (isfinite(xv) && isfinite(y)) { b1[2] += 1.0; b1[3] += xv; b1[4] += y; }
-    }
-    if (P.nc_out) P.nc_out[off + c] = y;
-  }
-  block_sums<5, NW>(b1, L.red);
-  const double stat_coh = b1[0] >= 1.0 ? b1[1] / b1[0] : nr_nan();
-  double stat_cc = nr_nan(), stat_ac = nr_nan();
-  if (P.disc_nc && P.out) {
-    const double mx = b1[3] / b1[2], my = b1[4] / b1[2];
-    double b2[4] = {0, 0, 0, 0};
-    for (int c = tid; c < k; c += BS) {
-      const double y = w[c], xv = P.disc_nc[off + c];
-      if (isfinite(xv) && isfinite(y)) {
-        const double dx = xv - mx, dy = y - my;
-        b2[0] += dx * dx;
-        b2[1] += dy * dy;
-        b2[2] += dx * dy;
-        b2[3] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
-      }
-    }
-    block_sums<4, NW>(b2, L.red);
-    stat_cc = b1[2] >= 1.0 ? b2[2] / (sqrt(b2[0]) * sqrt(b2[1])) : nr_nan();
-    stat_ac = b1[2] >= 1.0 ? b2[3] / b1[2] : nr_nan();
-  }
-  if (tid == 0) {
-    if (P.out) {
-      double* o = P.out + (int64_t)P.row_of[m] + (int64_t)P.n_rows * (int64_t)P.n_stat * p_local;
-      o[(int64_t)P.n_rows * P.slot_coherence] = na_fill(stat_coh);
-      o[(int64_t)P.n_rows * P.slot_cor_contrib] = na_fill(stat_cc);
-      o[(int64_t)P.n_rows * P.slot_avg_contrib] = na_fill(stat_ac);
-    }
-    if (P.coh_out) P.coh_out[m] = stat_coh;
-  }
-  __syncthreads();
-}
 
-// Next item from the persistent queue: (module m, local permutation, CSR
-// offset, k) and its index set in L.idx. Returns false when drained.
-template <int NW>
-__device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L, int* flags, int& m,
-                                          int64_t& p_local, int64_t& off, int& k) {
-  constexpr int BS = NW * 64;
-  const int tid = threadIdx.x;
-  if (tid == 0) flags[0] = atomicAdd(P.queue, 1);
-  __syncthreads();
-  const int item = flags[0];
-  __syncthreads();
-  if (item >= P.n_items) return false;
-  const int64_t mslot = item / P.n_perm;
-  p_local = item - mslot * P.n_perm;
-  m = P.mod_order[mslot];
-  off = P.node_off[m];
-  k = (int)(P.node_off[m + 1] - off);
-  nr_prp_key key;
-  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
-  for (int c = tid; c < k; c += BS) L.idx[c] = node_index(P.src, key, p_local, off + c);
-  if (tid == 0) flags[1] = 0;
-  __syncthreads();
-  return true;
-}
 
 // ---------------------------------------------------------------------------
 // Scheme 1 (global scratch): G in the workgroup's scratch slot, full (both
@@ -1249,7 +939,6 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   int m, k;
   int64_t p_local, off;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
-    if (P.fuse_net) net_item<NW, 4>(P.net, m, p_local, off, k, L.idx, L.red, part, kmax);
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     // ---- Gram [X 1]^T [X 1] on the matrix cores ----
     double g1[1] = {0.0};
@@ -1345,18 +1034,6 @@ __device__ __forceinline__ void rg_load4(const double* __restrict__ X, int o, in
   }
 }
 
-// Sum of a[r] over lane bits 0..3 (the 16 columns of a tile); lanes with
-// (lane & 3) == 0 end with the total of row group r = 2*b3 + b2, i.e. tile
-// row (lane >> 4) + 4r.
-__device__ __forceinline__ double rg_row_reduce(const double (&a)[4], int lane) {
-  const bool b3 = lane & 8, b2 = lane & 4;
-  const double v0 = (b3 ? a[2] : a[0]) + nr_dpp<NR_DPP_ROR8>(b3 ? a[0] : a[2]);
-  const double v1 = (b3 ? a[3] : a[1]) + nr_dpp<NR_DPP_ROR8>(b3 ? a[1] : a[3]);
-  double v = (b2 ? v1 : v0) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? v0 : v1);
-  v += nr_dpp<NR_DPP_XOR2>(v);
-  v += nr_dpp<NR_DPP_XOR1>(v);
-  return v;
-}
 
 // Per-wave tile range of the register scheme: ids [t0, t0 + n); the first
 // nreg = min(n, RG_RT) stay in registers, the remaining nl go to LDS.
@@ -1645,7 +1322,6 @@ module_profile_reg_kernel(ProfileParams P) {
   int m, k;
   int64_t p_local, off;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
-    if (P.fuse_net) net_item<NW>(P.net, m, p_local, off, k, L.idx, L.red, rowp, RG_KP);
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     const RgTiles R = rg_tiles(k, wave);
     const int kp = 16 * R.T;
@@ -1782,9 +1458,11 @@ __global__ void export_indices_kernel(IndexSource src, int64_t n_nodes_total, in
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-size_t net_kernel_lds(int k_max) {
-  return sizeof(double) * (8 * NR_WAVES + (size_t)NR_WAVES * k_max) + sizeof(uint32_t) * k_max;
-}
+// Four waves per item unless their per-wave weighted-degree copies would not
+// fit the LDS (modules of more than ~1,900 nodes): then two.
+int net_kernel_waves(int k_max) { return net_lds_bytes(4, k_max) <= 160 * 1024 ? 4 : 2; }
+
+size_t net_kernel_lds(int k_max) { return net_lds_bytes(net_kernel_waves(k_max), k_max); }
 
 // Compile-time module-size bucket of the packed kernel (0 = runtime layout).
 int packed_bucket(int k_max) { return k_max <= 320 ? 320 : 0; }
@@ -1817,7 +1495,11 @@ size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
 
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st) {
   const size_t lds = net_kernel_lds(P.k_max);
-  hipLaunchKernelGGL(module_net_kernel, dim3((unsigned)n_items), dim3(NR_BS), lds, st, P);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (net_kernel_waves(P.k_max) == 4)
+    hipLaunchKernelGGL(module_net_kernel<4>, dim3((unsigned)n_items), dim3(256), lds, st, P);
+  else
+    hipLaunchKernelGGL(module_net_kernel<2>, dim3((unsigned)n_items), dim3(128), lds, st, P);
   return hipGetLastError();
 }
 

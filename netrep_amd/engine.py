@@ -82,7 +82,10 @@ class Engine:
         self.n_samples = s
 
     def set_dataset_device(self, corr_ptr: int, net_ptr: int, data_ptr, n_nodes: int, n_samples: int):
-        """Device pointers (e.g. torch tensors after an RCCL broadcast)."""
+        """Device pointers (e.g. torch tensors after an RCCL broadcast). The
+        engine reads them on its own stream: the producer's work must be
+        complete (e.g. torch.cuda.synchronize()) -- torch's streams belong to
+        its own HIP runtime and are not ordered with the engine's."""
         self._check(self._lib.nr_set_dataset(self._h, C.cast(corr_ptr, L._dp), C.cast(net_ptr, L._dp),
                                              C.cast(data_ptr, L._dp) if data_ptr else None,
                                              n_nodes, n_samples, L.NR_DEVICE))

@@ -105,3 +105,19 @@ def torch_dataset(layout: Layout, n_samples: int, seed: int, preserve_all: bool 
     corr.diagonal().fill_(1.0)
     net = corr.abs().pow(5)
     return xt, corr, net
+
+
+def scale_rows_torch(x):
+    """Scale (src/scale.cpp:21) applied to genes stored as rows of x (N x S):
+    (x - mean) / sd with n-1 normalisation, on the tensor's device."""
+    mu = x.mean(dim=1, keepdim=True)
+    sd = x.std(dim=1, unbiased=True, keepdim=True)
+    return (x - mu) / sd
+
+
+def csr_of(layout: Layout):
+    """(node_off, idx) of the layout's modules in `modules` order (CSR)."""
+    mods = layout.modules
+    node_off = np.concatenate([[0], np.cumsum([layout.members[m].size for m in mods])]).astype(np.int64)
+    idx = np.concatenate([layout.members[m] for m in mods]).astype(np.int32)
+    return node_off, idx

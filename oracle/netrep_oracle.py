@@ -102,10 +102,25 @@ def sign_aware_mean(v1, v2):
     return float(np.mean(np.sign(v1[cc]) * v2[cc]))
 
 
+def arma_accumulate(a, axis=0):
+    """arma::sum along `axis` as Armadillo computes it (arrayops::accumulate /
+    op_sum's proxy loop, RcppArmadillo, unvendored): two sequential
+    accumulators over the even and odd positions, returned as acc1 + acc2.
+    np.cumsum is a sequential left-to-right sum, so its last element is the
+    accumulator's value."""
+    a = np.moveaxis(np.asarray(a, dtype=np.float64), axis, 0)
+    if a.shape[0] == 0:
+        return np.zeros(a.shape[1:])
+    acc1 = np.cumsum(a[0::2], axis=0)[-1]
+    acc2 = np.cumsum(a[1::2], axis=0)[-1] if a.shape[0] > 1 else np.zeros(a.shape[1:])
+    return acc1 + acc2
+
+
 def weighted_degree(net, idx_sorted):
-    """WeightedDegree src/netStats.cpp:124-144: colsum(|net[idx,idx]|) - |diag[idx]|."""
+    """WeightedDegree src/netStats.cpp:124-144: colsum(|net[idx,idx]|) - |diag[idx]|,
+    the column sums in Armadillo's order with the diagonal included (:135)."""
     sub = np.abs(net[np.ix_(idx_sorted, idx_sorted)])
-    return sub.sum(axis=0) - np.abs(net[idx_sorted, idx_sorted])
+    return arma_accumulate(sub, axis=0) - np.abs(net[idx_sorted, idx_sorted])
 
 
 def average_edge_weight(wd):
@@ -113,8 +128,9 @@ def average_edge_weight(wd):
     k = np.uint32(len(wd))
     with np.errstate(over="ignore"):
         pairs = float(np.uint32(k * k - k))
+    total = float(arma_accumulate(np.asarray(wd, dtype=np.float64))) if len(wd) else 0.0
     with np.errstate(invalid="ignore", divide="ignore"):
-        return float(np.sum(wd)) / pairs if pairs != 0 else (np.nan if np.sum(wd) == 0 else np.inf)
+        return total / pairs if pairs != 0 else (np.nan if total == 0 else np.inf)
 
 
 def corr_vector(corr, idx):

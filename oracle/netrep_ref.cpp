@@ -19,7 +19,9 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <functional>
 #include <cstdint>
 #include <cstring>
 #include <numeric>
@@ -68,15 +70,33 @@ void sort_nodes(const std::vector<int64_t>& idx, std::vector<int64_t>& sorted, s
   }
 }
 
-// WeightedDegree src/netStats.cpp:124-144 on sorted indices, then reordered by rank
+// arma::sum of a column / vector: Armadillo's arrayops::accumulate (also
+// op_sum's proxy loop), two accumulators over the even and odd positions,
+// returned as acc1 + acc2 (RcppArmadillo, unvendored, version unpinned:
+// DESCRIPTION:28). The order matters for WeightedDegree: its column sums
+// include the diagonal (src/netStats.cpp:135-141).
+template <class F>
+double arma_accumulate(size_t n, F at) {
+  double acc1 = 0.0, acc2 = 0.0;
+  size_t j = 1;
+  for (; j < n; j += 2) {
+    acc1 += at(j - 1);
+    acc2 += at(j);
+  }
+  if (j - 1 < n) acc1 += at(j - 1);
+  return acc1 + acc2;
+}
+
+// WeightedDegree src/netStats.cpp:124-144 on sorted indices: colsum of
+// |net(srt, srt)| (diagonal included), minus |diag|; reordered by rank
+// (src/permutations.cpp:81-82)
 void weighted_degree(const double* net, int64_t n, const std::vector<int64_t>& srt,
                      const std::vector<size_t>& rank, std::vector<double>& wd) {
   const size_t k = srt.size();
   std::vector<double> ws(k);
   for (size_t j = 0; j < k; ++j) {
-    double s = 0.0;
     const double* col = net + srt[j] * n;
-    for (size_t i = 0; i < k; ++i) s += std::fabs(col[srt[i]]);
+    const double s = arma_accumulate(k, [&](size_t i) { return std::fabs(col[srt[i]]); });
     ws[j] = s - std::fabs(col[srt[j]]);
   }
   wd.resize(k);
@@ -86,9 +106,7 @@ void weighted_degree(const double* net, int64_t n, const std::vector<int64_t>& s
 double average_edge_weight(const std::vector<double>& wd) {  // src/netStats.cpp:154-162
   const uint32_t k = (uint32_t)wd.size();
   const double pairs = (double)(uint32_t)(k * k - k);
-  double s = 0.0;
-  for (double x : wd) s += x;
-  return s / pairs;
+  return arma_accumulate(wd.size(), [&](size_t i) { return wd[i]; }) / pairs;
 }
 
 double pearson(const double* a, const double* b, size_t n) {
@@ -254,17 +272,41 @@ int ref_permutation_procedure(const double* data, const double* corr, const doub
   }
   const double na = na_real();
   const int64_t slice = (int64_t)n_rows * P.n_stat;
+  n_threads = std::max(1, n_threads);
+  // Independent (permutation, module) items over threads: used for the
+  // observed statistics and, with explicit shuffles and fewer permutations
+  // than threads, for the nulls (checker mode; results are per item, so the
+  // split does not change them).
+  auto run_items = [&](int64_t n_items, const std::function<void(int64_t)>& item) {
+    std::atomic<int64_t> next{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t)
+      th.emplace_back([&]() {
+        for (int64_t i = next++; i < n_items; i = next++) item(i);
+      });
+    for (auto& x : th) x.join();
+  };
   if (observed) {
     std::fill(observed, observed + slice, na);
-    for (int m = 0; m < n_present; ++m) {
+    run_items(n_present, [&](int64_t m) {
       std::vector<int64_t> idx(test_idx + node_off[m], test_idx + node_off[m + 1]);
-      module_stats(P, m, idx, observed + row_of[m], n_rows);
-    }
+      module_stats(P, (int)m, idx, observed + row_of[m], n_rows);
+    });
     for (int64_t i = 0; i < slice; ++i) if (!std::isfinite(observed[i])) observed[i] = na;
   }
   if (n_perm <= 0 || !nulls) return 0;
   std::fill(nulls, nulls + slice * n_perm, na);
-  n_threads = std::max(1, n_threads);
+  if (pi && n_perm < n_threads) {
+    run_items(n_perm * n_present, [&](int64_t it) {
+      const int64_t p = it / n_present;
+      const int m = (int)(it % n_present);
+      std::vector<int64_t> idx;
+      for (int64_t c = node_off[m]; c < node_off[m + 1]; ++c) idx.push_back(null_idx[pi[p * n_null + null_pos[c]]]);
+      module_stats(P, m, idx, nulls + p * slice + row_of[m], n_rows);
+    });
+    for (int64_t i = 0; i < slice * n_perm; ++i) if (!std::isfinite(nulls[i])) nulls[i] = na;
+    return 0;
+  }
   // contiguous chunks, remainder to the first threads (src/permutations.cpp:338-354)
   std::vector<int64_t> start(n_threads + 1, 0);
   for (int t = 0; t < n_threads; ++t)

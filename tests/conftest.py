@@ -58,5 +58,7 @@ def assert_stats_close(got, exp, rtol=RTOL, floor=FLOOR, what=""):
     assert (np.sign(got[~gf & ~np.isnan(got)]) == np.sign(exp[~ef & ~np.isnan(exp)])).all(), what
     err = np.abs(got[gf] - exp[ef]) / np.maximum(np.abs(exp[ef]), floor)
     if err.size:
-        assert err.max() <= rtol, f"{what}: max scaled error {err.max():.3e} at {np.argmax(err)}"
+        at = tuple(int(i) for i in np.argwhere(gf)[np.argmax(err)])
+        assert err.max() <= rtol, (f"{what}: max scaled error {err.max():.3e} at index {at}: "
+                                   f"got {got[at]!r}, expected {exp[at]!r}")
     return float(err.max()) if err.size else 0.0

@@ -1,0 +1,270 @@
+"""GPU parity at the BASELINE.json configurations' real sizes.
+
+Each case runs the HIP engine and the C++ CPU restatement of the reference
+(oracle/netrep_ref.cpp: CorrVector / WeightedDegree / LAPACK dgesvd summary
+profile, src/netStats.cpp) on IDENTICAL shuffles -- the keyed permutations of
+the run exported with nr_prp_table -- and compares every statistic at the
+north-star bar: |gpu - oracle| <= 1e-10 * max(|oracle|, 1e-2), NA patterns
+bit for bit (conftest.assert_stats_close).
+
+  C2  5,000 genes x 100 samples, 20 modules (30-300), 256 permutations
+  C3  20,000 genes x 500 samples, 50 modules (30-300) -- the metric's
+      workload -- on a 64-permutation sample (3,200 eigenproblems at S = 500),
+      plus the discovery vectors (IntermediateProperties) against the numpy
+      oracle
+  C4  the network-only path on the same 20,000-gene matrices, 256 permutations
+  C5  40,000 genes x 1,000 samples, 40 modules (30-2,000, so k > S), three
+      test datasets run back to back through netrep_PermutationProcedure with
+      null = "all" over a pool (40,000 test genes) larger than the discovery
+      assignments (30,000 genes), 3 permutations per dataset
+
+The largest scaled error of every case is written to
+gpurun_out/parity_maxerr.json (the record quoted in DESIGN.md).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import netrep_amd as N
+from netrep_amd import synthetic as S
+from netrep_amd.api import RMatrix
+from oracle import netrep_oracle as O
+from oracle import ref_cpp
+
+from conftest import ROOT, assert_stats_close
+
+pytestmark = pytest.mark.gpu
+
+ORACLE_THREADS = 16
+REPORT = {}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _report():
+    yield
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    path = os.path.join(out, "parity_maxerr.json")
+    old = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f)
+    old.update(REPORT)
+    with open(path, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
+
+
+def record(name, err, **extra):
+    REPORT[name] = dict(max_scaled_error=err, **extra)
+    print(f"{name}: max scaled error {err:.3e} {extra}")
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class Case:
+    """A synthetic configuration built on the GPU exactly as bench.py builds it."""
+
+    def __init__(self, cfg, seed):
+        torch = _torch()
+        n, s, sizes, _, with_data = S.CONFIGS[cfg]
+        self.n, self.s, self.sizes = n, s, sizes
+        self.lay = S.make_layout(n, sizes, seed)
+        self.node_off, self.idx = S.csr_of(self.lay)
+        dev = torch.device("cuda", 0)
+        # discovery vectors on the device (IntermediateProperties)
+        dx, dc, dn = S.torch_dataset(self.lay, s, seed + 1, device=dev)
+        dxs = S.scale_rows_torch(dx).contiguous()
+        del dx
+        torch.cuda.synchronize()   # torch's stream belongs to another HIP runtime: finish before the engine reads
+        eng = N.Engine(0)
+        eng.set_dataset_device(dc.data_ptr(), dn.data_ptr(), dxs.data_ptr(), n, s)
+        self.disc = eng.module_vectors(self.node_off, self.idx, True)
+        self.disc_host = None
+        if cfg == "C3":   # kept for the discovery-vector check
+            self.disc_host = (dxs.cpu().numpy().T, dc.cpu().numpy().T, dn.cpu().numpy().T)
+        eng.close()
+        del dxs, dc, dn
+        torch.cuda.empty_cache()
+        tx, tc, tn = S.torch_dataset(self.lay, s, seed + 2, preserve_all=False, device=dev)
+        txs = S.scale_rows_torch(tx).contiguous()
+        del tx
+        torch.cuda.synchronize()
+        self.eng = N.Engine(0)
+        self.eng.set_dataset_device(tc.data_ptr(), tn.data_ptr(), txs.data_ptr(), n, s)
+        self.mods = list(range(len(self.lay.modules)))
+        self.eng.set_modules(len(self.mods), self.mods, self.node_off, self.idx, self.idx,
+                             self.disc["corr"], self.disc["degree"], self.disc["contribution"])
+        self.eng.set_null_pool(np.arange(n, dtype=np.int32))
+        self.eng_nodata = N.Engine(0)
+        self.eng_nodata.set_dataset_device(tc.data_ptr(), tn.data_ptr(), 0, n, 0)
+        self.eng_nodata.set_modules(len(self.mods), self.mods, self.node_off, self.idx, self.idx,
+                                    self.disc["corr"], self.disc["degree"], None)
+        self.eng_nodata.set_null_pool(np.arange(n, dtype=np.int32))
+        # bitwise-symmetric matrices: the transposed view is the column-major
+        # array without a host copy
+        self.tc = tc.cpu().numpy().T
+        self.tn = tn.cpu().numpy().T
+        self.txs = txs.cpu().numpy().T      # S x N, column-major view
+        del tc, tn, txs
+        torch.cuda.empty_cache()
+
+    def oracle(self, p0, p1, seed, with_data):
+        pis = N.prp_table(seed, p0, p1, self.n)
+        return ref_cpp.permutation_procedure(
+            self.txs if with_data else None, self.tc, self.tn, len(self.mods), self.mods, self.node_off,
+            self.idx, self.idx, np.arange(self.n), self.disc["corr"], self.disc["degree"],
+            self.disc["contribution"] if with_data else None, p1 - p0, pi=pis, n_threads=ORACLE_THREADS)
+
+    def close(self):
+        self.eng.close()
+        self.eng_nodata.close()
+
+
+@pytest.fixture(scope="module")
+def c3():
+    c = Case("C3", 0x5EED)
+    yield c
+    c.close()
+
+
+def test_c3_discovery_vectors_vs_numpy_oracle(c3):
+    """IntermediateProperties (src/discProps.cpp:92-122) of all 50 modules at
+    20,000 x 500: CorrVector, weighted degree and node contributions."""
+    dxs, dc, dn = c3.disc_host
+    errs = []
+    o = 0
+    ocv = 0
+    for m in c3.lay.modules:
+        idx = c3.lay.members[m]
+        k = idx.size
+        exp = O.intermediate_properties(dxs, dc, dn, {m: idx})
+        errs.append(assert_stats_close(c3.disc["corr"][ocv:ocv + k * (k - 1) // 2], exp["corr"][m], what=f"corr {m}"))
+        errs.append(assert_stats_close(c3.disc["degree"][o:o + k], exp["degree"][m], what=f"degree {m}"))
+        errs.append(assert_stats_close(c3.disc["contribution"][o:o + k], exp["contribution"][m],
+                                       what=f"contribution {m}"))
+        o += k
+        ocv += k * (k - 1) // 2
+    record("C3 discovery vectors (50 modules)", max(errs))
+
+
+def test_c3_nulls_vs_cpp_oracle(c3):
+    """64 permutations x 50 modules of the metric's workload (3,200 summary
+    profiles at S = 500) plus the observed statistics."""
+    seed, p0 = 0x5EED, 123_456
+    got = c3.eng.run(p0, p0 + 64, seed)
+    exp, obs = c3.oracle(p0, p0 + 64, seed, True)
+    e1 = assert_stats_close(c3.eng.observed(), obs, what="C3 observed")
+    e2 = assert_stats_close(got, exp, what="C3 nulls")
+    record("C3 nulls (64 perms x 50 modules, S=500)", max(e1, e2), perms=64)
+
+
+def test_c4_network_only_full_size(c3):
+    """permutationsNoData at 20,000 nodes: 256 permutations x 50 modules."""
+    seed, p0 = 77, 9_000
+    got = c3.eng_nodata.run(p0, p0 + 256, seed)
+    exp, obs = c3.oracle(p0, p0 + 256, seed, False)
+    e1 = assert_stats_close(c3.eng_nodata.observed(), obs, what="C4 observed")
+    e2 = assert_stats_close(got, exp, what="C4 nulls")
+    record("C4 nulls (256 perms x 50 modules, network only)", max(e1, e2), perms=256)
+
+
+def test_c2_exact_shape():
+    """5,000 genes x 100 samples, 20 modules of 30-300 genes (most k > S)."""
+    c = Case("C2", 1002)
+    try:
+        seed, p0 = 42, 0
+        got = c.eng.run(p0, p0 + 256, seed)
+        exp, obs = c.oracle(p0, p0 + 256, seed, True)
+        e1 = assert_stats_close(c.eng.observed(), obs, what="C2 observed")
+        e2 = assert_stats_close(got, exp, what="C2 nulls")
+        record("C2 nulls (256 perms x 20 modules, S=100)", max(e1, e2), perms=256)
+    finally:
+        c.close()
+
+
+# ---------------------------------------------------------------------------
+# C5: 40k genes x 1000 samples, modules up to 2000 genes, 3 test datasets,
+# null = "all" through the reference interface (names, MakeNullMap)
+# ---------------------------------------------------------------------------
+
+def _c5_names(n):
+    return [f"G{i}" for i in range(n)]
+
+
+def test_c5_three_datasets_null_all():
+    torch = _torch()
+    n, s, sizes, _, _ = S.CONFIGS["C5"]
+    seed = 1005
+    n_disc = 30_000
+    rng = np.random.default_rng(seed)
+    all_names = _c5_names(n)
+    # discovery: 30,000 of the 40,000 genes, modules over them, the rest background
+    disc_pos = np.sort(rng.choice(n, n_disc, replace=False))
+    lay_d = S.make_layout(n_disc, sizes, seed)
+    d_names = [all_names[i] for i in disc_pos]
+    ma = dict(zip(d_names, lay_d.labels))
+    modules = lay_d.modules
+    dev = torch.device("cuda", 0)
+    dx, dc, dn = S.torch_dataset(lay_d, s, seed + 1, device=dev)
+    dxs = S.scale_rows_torch(dx).contiguous()
+    del dx
+    torch.cuda.synchronize()
+    eng = N.Engine(0)
+    eng.set_dataset_device(dc.data_ptr(), dn.data_ptr(), dxs.data_ptr(), n_disc, s)
+    node_off, idx = S.csr_of(lay_d)
+    v = eng.module_vectors(node_off, idx, True)
+    eng.close()
+    del dxs, dc, dn
+    torch.cuda.empty_cache()
+    disc = {"degree": {}, "corr": {}, "contribution": {}}
+    o = ocv = 0
+    for m in modules:
+        k = lay_d.members[m].size
+        disc["degree"][m] = v["degree"][o:o + k]
+        disc["contribution"][m] = v["contribution"][o:o + k]
+        disc["corr"][m] = v["corr"][ocv:ocv + k * (k - 1) // 2]
+        o += k
+        ocv += k * (k - 1) // 2
+    errs = []
+    for t in range(3):
+        # test dataset t: all 40,000 genes in a dataset-specific column order;
+        # its modules are the discovery modules (mapped through the names)
+        order = np.random.default_rng(seed + 10 + t).permutation(n)
+        t_names = [all_names[i] for i in order]
+        pos_of = {nm: j for j, nm in enumerate(t_names)}
+        lay_t = S.Layout(n, sizes, t_names, ["0"] * n, modules,
+                         {m: np.sort(np.array([pos_of[d_names[i]] for i in lay_d.members[m]]))
+                          for m in modules})
+        tx, tc, tn = S.torch_dataset(lay_t, s, seed + 20 + t, preserve_all=(t == 0), device=dev)
+        txs = S.scale_rows_torch(tx)
+        del tx
+        tcn, tnn = tc.cpu().numpy().T, tn.cpu().numpy().T   # symmetric: column-major views
+        txn = np.asfortranarray(txs.cpu().numpy().T)
+        del tc, tn, txs
+        torch.cuda.empty_cache()
+        n_perm, pseed = 3, 500 + t
+        res = N.PermutationProcedure(disc, RMatrix(txn, None, t_names), RMatrix(tcn, t_names, t_names),
+                                     RMatrix(tnn, t_names, t_names), ma, modules, n_perm,
+                                     nullHypothesis="all", seed=pseed)
+        # oracle on the same resolved index sets (MakeNullMap over test names for "all")
+        mi = O.ModuleIndex(list(ma), list(ma.values()), t_names, modules, null="all")
+        assert mi.null_idx.size == n > n_disc
+        mods = mi.mods_present
+        noff = np.concatenate([[0], np.cumsum([mi.test_idx[m].size for m in mods])])
+        pis = N.prp_table(pseed, 0, n_perm, mi.null_idx.size)
+        exp, obs = ref_cpp.permutation_procedure(
+            txn, tcn, tnn, len(modules), [modules.index(m) for m in mods], noff,
+            np.concatenate([mi.test_idx[m] for m in mods]), np.concatenate([mi.null_pos[m] for m in mods]),
+            mi.null_idx, np.concatenate([disc["corr"][m] for m in mods]),
+            np.concatenate([disc["degree"][m] for m in mods]),
+            np.concatenate([disc["contribution"][m] for m in mods]), n_perm, pi=pis, n_threads=ORACLE_THREADS)
+        errs.append(assert_stats_close(res["observed"], obs, what=f"C5 dataset {t} observed"))
+        errs.append(assert_stats_close(res["nulls"], exp, what=f"C5 dataset {t} nulls"))
+        del tcn, tnn, txn
+    record("C5 (3 test datasets x 3 perms x 40 modules, null=all, S=1000, k<=2000)", max(errs),
+           datasets=3, perms_per_dataset=3)

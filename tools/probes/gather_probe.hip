@@ -1,0 +1,78 @@
+// Microbenchmark: the random-access ceiling of the network-statistics gather.
+// A module's pairs read corr/net(idx[ii], idx[jj]) as ONE 16-byte element of
+// the interleaved N x N double2 matrix at a random (row, column): every read
+// touches its own cache line. This measures, chip-wide, how many such random
+// 16-byte reads per second MI355X sustains from a matrix far larger than the
+// Infinity Cache (N = 20,000: 6.4 GB), for several loads in flight per
+// thread, and the same for 8-byte reads (one of the two matrices alone).
+// Output: reads/s and useful GB/s (the ceiling DESIGN.md quotes for the net
+// kernel's roofline).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+template <int U, typename T>
+__global__ void gather(const T* __restrict__ a, int64_t n, int iters, double* out) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  double acc = 0.0;
+  for (int it = 0; it < iters; ++it) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t h1 = hash32(tid * 7919u + (uint32_t)(it * U + u) * 104729u);
+      const uint32_t h2 = hash32(h1 ^ 0x9E3779B9u);
+      const int64_t r = h1 % (uint32_t)n, c = h2 % (uint32_t)n;
+      v[u] = a[r + c * n];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (sizeof(T) == 16) acc += ((const double*)&v[u])[0] + ((const double*)&v[u])[1];
+      else acc += (double)v[u];
+    }
+  }
+  if (acc == 1234.5) out[tid] = acc;
+}
+
+template <int U, typename T>
+void run(const void* buf, int64_t n, int blocks, int threads, int iters, double* out, const char* name) {
+  hipLaunchKernelGGL((gather<U, T>), dim3(blocks), dim3(threads), 0, 0, (const T*)buf, n, iters, out);
+  hipDeviceSynchronize();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL((gather<U, T>), dim3(blocks), dim3(threads), 0, 0, (const T*)buf, n, iters, out);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  const double reads = (double)blocks * threads * iters * U;
+  printf("%-8s U=%2d blocks=%5d x %4d: %.3f ms  %.2f G reads/s  %.1f GB/s useful\n", name, U, blocks, threads,
+         ms, reads / (ms * 1e-3) / 1e9, reads * sizeof(T) / (ms * 1e-3) / 1e9);
+}
+
+int main() {
+  const int64_t n = 20000;
+  void* buf = nullptr;
+  if (hipMalloc(&buf, (size_t)(n * n) * 16) != hipSuccess) return 1;
+  hipMemset(buf, 0, (size_t)(n * n) * 16);
+  double* out;
+  hipMalloc(&out, sizeof(double) * (1 << 24));
+  // 256 CUs x 8 blocks x 256 threads
+  run<4, double2>(buf, n, 2048, 256, 64, out, "16B");
+  run<8, double2>(buf, n, 2048, 256, 32, out, "16B");
+  run<16, double2>(buf, n, 2048, 256, 16, out, "16B");
+  run<8, double2>(buf, n, 4096, 256, 16, out, "16B");
+  run<8, double2>(buf, n, 1024, 256, 64, out, "16B");
+  run<8, double>(buf, n, 2048, 256, 32, out, "8B");
+  run<16, double>(buf, n, 2048, 256, 16, out, "8B");
+  // one 512-thread block per CU, 4 in flight (the fused profile kernel's budget)
+  run<4, double2>(buf, n, 256, 512, 64, out, "16B/1wg");
+  run<8, double2>(buf, n, 256, 512, 32, out, "16B/1wg");
+  return 0;
+}
