@@ -24,11 +24,10 @@ __device__ __forceinline__ double na_fill(double x) {
   return isfinite(x) ? x : __longlong_as_double(0x7FF00000000007A2ll);
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+__device__ __forceinline__ double nr_wave_sum(double v);
+__device__ __forceinline__ double nr_wave_max(double v);
+// Wave-wide sum (every lane active); register butterflies, see nr_wave_sum.
+__device__ __forceinline__ double wave_sum(double v) { return nr_wave_sum(v); }
 
 // Block-wide sums of N values; result broadcast to every thread. `red` must
 // hold N * NR_WAVES doubles of LDS. Contains two barriers.
@@ -109,7 +108,16 @@ __device__ __forceinline__ double nr_rcp(double d) {
 // normalised matrix, p_i = (a_i - x) p_{i-1} - b_{i-1}^2 p_{i-2} (sign changes
 // of p_0..p_n = eigenvalues below x): one FMA on the dependency chain per
 // step and no division; |p| is renormalised every 4 steps.
-static __device__ double tri_top_eigenvalue(const double* alpha, const double* beta, int n, int lane) {
+//
+// Warm start (r_prev > 0): theta_prev, the top Ritz value of an earlier
+// check, is a lower bound (Cauchy interlacing), and its Ritz residual r_prev
+// bounds the distance to an eigenvalue of the grown matrix, so the top one
+// lies in [theta_prev, theta_prev + r_prev] unless the first pass -- whose
+// last lane sits exactly on that upper end -- finds eigenvalues above it;
+// then the search continues to the Gershgorin bound. Near convergence this
+// halves the passes of a check.
+static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha, const double* beta, int n, int lane,
+                                                            double theta_prev = 0.0, double r_prev = 0.0) {
   double lo = alpha[0], hi = alpha[0];
   for (int i = lane; i < n; i += 64) {
     const double r = (i > 0 ? fabs(beta[i - 1]) : 0.0) + (i < n - 1 ? fabs(beta[i]) : 0.0);
@@ -125,8 +133,17 @@ static __device__ double tri_top_eigenvalue(const double* alpha, const double* b
   const double inv = 1.0 / scale;
   lo -= 1e-14 * scale;
   hi += 1e-14 * scale;
-  for (int it = 0; it < 12; ++it) {
-    const double x = (lo + (hi - lo) * (double)(lane + 1) / 65.0) * inv;
+  const double g_hi = hi;
+  bool warm = r_prev > 0.0 && isfinite(r_prev) && theta_prev - 4e-16 * scale > lo &&
+              theta_prev + 1.01 * r_prev + 4e-16 * scale < hi;
+  if (warm) {
+    lo = theta_prev - 4e-16 * scale;
+    hi = theta_prev + 1.01 * r_prev + 4e-16 * scale;
+  }
+  for (int it = 0; it < 14; ++it) {
+    // warm first pass: 64 points ending on hi; otherwise 64 interior points
+    const double den = warm ? 64.0 : 65.0;
+    const double x = (lo + (hi - lo) * (double)(lane + 1) / den) * inv;
     double p0 = 1.0, p1 = alpha[0] * inv - x;
     int cnt = p1 < 0.0;  // eigenvalues < x
 #pragma unroll 4
@@ -147,10 +164,17 @@ static __device__ double tri_top_eigenvalue(const double* alpha, const double* b
     const unsigned long long below = __ballot(cnt <= n - 1);
     // lanes are ordered by x: lanes [0, t) have cnt <= n-1, lanes [t, 64) have cnt == n
     const int t = __popcll(below);
-    const double xlo = lo + (hi - lo) * (double)t / 65.0;
-    const double xhi = lo + (hi - lo) * (double)(t + 1) / 65.0;
+    if (warm && t == 64) {  // eigenvalues above the residual bound: cold search above it
+      lo = hi;
+      hi = g_hi;
+      warm = false;
+      continue;
+    }
+    const double xlo = lo + (hi - lo) * (double)t / den;
+    const double xhi = lo + (hi - lo) * (double)(t + 1) / den;
     lo = xlo;
     hi = xhi;
+    warm = false;
     if (hi - lo <= 2e-16 * scale) break;
   }
   return 0.5 * (lo + hi);
@@ -162,7 +186,7 @@ static __device__ double tri_top_eigenvalue(const double* alpha, const double* b
 // of an unreduced Jacobi matrix is positive and its tail decays once the
 // pair converges, so upward it is the dominant (stable) solution. rb holds
 // 1/beta[0..n-1), one wave fills it. Returns beta_j / |y| (lane 0).
-static __device__ double tri_top_resid(const double* alpha, const double* beta, int n, double theta, double beta_j,
+static __device__ __forceinline__ double tri_top_resid(const double* alpha, const double* beta, int n, double theta, double beta_j,
                                 double* rb, int lane) {
   for (int i = lane; i < n - 1; i += 64) rb[i] = 1.0 / beta[i];
   __builtin_amdgcn_wave_barrier();
@@ -186,7 +210,7 @@ static __device__ double tri_top_resid(const double* alpha, const double* beta, 
 // Eigenvector of the tridiagonal for eigenvalue theta by two steps of inverse
 // iteration; LU with partial pivoting as LAPACK dgttrf/dgtts2. Single lane.
 // y[0..n) comes back normalised; work holds 5n doubles.
-static __device__ void tri_eigenvector(const double* alpha, const double* beta, int n, double theta,
+static __device__ __forceinline__ void tri_eigenvector(const double* alpha, const double* beta, int n, double theta,
                                 double* y, double* work) {
   double* dl = work;
   double* d = work + n;
@@ -276,9 +300,7 @@ __device__ __forceinline__ double omega_update(const double* alpha, const double
     om_next[j + 1] = 1.0;
     mx = fmax(mx, fabs(om_next[j]));
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-  return mx;
+  return nr_wave_max(mx);
 }
 
 // Cross-lane butterfly steps without LDS (gfx950): v_permlane32_swap /
@@ -306,6 +328,34 @@ constexpr int NR_DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
 constexpr int NR_DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
 constexpr int NR_DPP_ROR8 = 0x128;        // row_ror:8 == lane ^ 8 within a row
 constexpr int NR_DPP_HALF_MIRROR = 0x141; // lane ^ 7 within 8 lanes (flips bit 2)
+
+// Wave-wide sum / max in registers (DPP within 16-lane rows, permlane swaps
+// across rows; no LDS round trips). Every lane ends with the same value.
+__device__ __forceinline__ double nr_wave_sum(double v) {
+  v += nr_dpp<NR_DPP_XOR1>(v);
+  v += nr_dpp<NR_DPP_XOR2>(v);
+  v += nr_dpp<NR_DPP_HALF_MIRROR>(v);  // quads are uniform: lane ^ 4
+  v += nr_dpp<NR_DPP_ROR8>(v);
+  v = nr_swap16_sum(v, v);
+  return nr_swap32_sum(v, v);
+}
+__device__ __forceinline__ double nr_swap16_max(double x) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(x), false, false);
+  return fmax(__hiloint2double((int)hi[0], (int)lo[0]), __hiloint2double((int)hi[1], (int)lo[1]));
+}
+__device__ __forceinline__ double nr_swap32_max(double x) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(x), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(x), false, false);
+  return fmax(__hiloint2double((int)hi[0], (int)lo[0]), __hiloint2double((int)hi[1], (int)lo[1]));
+}
+__device__ __forceinline__ double nr_wave_max(double v) {
+  v = fmax(v, nr_dpp<NR_DPP_XOR1>(v));
+  v = fmax(v, nr_dpp<NR_DPP_XOR2>(v));
+  v = fmax(v, nr_dpp<NR_DPP_HALF_MIRROR>(v));
+  v = fmax(v, nr_dpp<NR_DPP_ROR8>(v));
+  return nr_swap32_max(nr_swap16_max(v));
+}
 
 // Transpose-reduce of 16 per-lane column partials up[0..16) over the 64 rows
 // (lanes) of a unit: afterwards lanes with (lane & 3) == 0 hold the column

@@ -69,6 +69,7 @@ struct nr_ctx {
   double* d_disc_nc = nullptr;
   double* d_cv_shift = nullptr;
   int32_t* d_mod_order = nullptr;
+  std::vector<int32_t> order_k_h;  // module sizes in d_mod_order's order (descending)
 
   // null pool
   int32_t* d_null_idx = nullptr;
@@ -174,29 +175,48 @@ int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
 
 // Launch plan of the summary-profile kernel. Default: the packed symmetric
 // Gram in global scratch, 4-wave workgroups, 3 per CU (variant 2; measured
-// fastest at C3: 23.4 ms per 256 permutations). Alternatives for A/B:
+// fastest at C3: 23.2 ms per 256 permutations). Alternatives for A/B: the
+// register-resident 4-wave kernel for modules of <= 255 nodes (variant 5,
+// kernels_rg4.hip; larger modules of the same launch go to variant 2),
 // the register-resident Gram (variant 3, one 8-wave workgroup per CU, the
 // Gram never leaves the registers/LDS of the CU that computed it; modules of
 // <= 303 nodes; 30.5 ms), packed 8-wave (1) and full Gram (0, also the
 // fallback when the packed layout does not fit LDS):
-// NETREP_PROFILE_VARIANT=reg|packed4|packed|full, NETREP_PROFILE_WG_PER_CU.
+// NETREP_PROFILE_VARIANT=rg4|reg|packed4|packed|full, NETREP_PROFILE_WG_PER_CU
+// (a non-rg4 value applies to every module).
 struct ProfilePlan {
-  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave, 3 register-resident,
-                    // 4 full Gram with the matvec partials in global scratch (large modules)
+  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave, 3 register-resident (8 waves),
+                    // 4 full Gram with the matvec partials in global scratch (large modules),
+                    // 5 register-resident 4-wave (kernels_rg4.hip, the default for k <= 303)
   int slots = 0;
   int per_cu = 1;
   int64_t gram_doubles = 0, stride = 0;
 };
 
-int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, ProfilePlan* plan) {
+// NETREP_PROFILE_VARIANT (A/B runs): -1 when unset.
+int profile_variant_env() {
+  const char* f = std::getenv("NETREP_PROFILE_VARIANT");
+  if (!f) return -1;
+  const std::string v(f);
+  return v == "packed" ? 1 : v == "full" ? 0 : v == "reg" ? 3 : v == "packed4" ? 2 : v == "rg4" ? 5 : -1;
+}
+
+// rg4: plan the register-resident 4-wave kernel (variant 5; the caller
+// guarantees k_max <= rg4_kernel_k_max()).
+int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg4, ProfilePlan* plan) {
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
   const int m = profile_m_max(k_max);
-  int variant = 2;
-  if (const char* f = std::getenv("NETREP_PROFILE_VARIANT")) {
-    const std::string v(f);
-    variant = v == "packed" ? 1 : v == "full" ? 0 : v == "reg" ? 3 : 2;
+  if (rg4) {
+    plan->variant = 5;
+    plan->per_cu = 1;
+    plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, dev_cu));
+    plan->gram_doubles = 0;  // the Gram lives in registers / LDS
+    plan->stride = (int64_t)nr::kRg4StepCap * k_max;  // Lanczos basis columns beyond the LDS share
+    return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
   }
+  const int forced = profile_variant_env();
+  int variant = forced >= 0 && forced != 5 ? forced : 2;
   if (variant == 3 && k_max > nr::reg_kernel_k_max()) variant = 2;
   if (variant != 0 && nr::profile_kernel_lds(k_max, m, n_samples, variant) > 160 * 1024) variant = 0;
   // Large modules: the per-wave matvec partials (4 x k doubles) move from LDS
@@ -225,6 +245,56 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   }
   plan->stride = plan->gram_doubles + (int64_t)k_max * m + (variant == 4 ? (int64_t)nr::kProfileWaves * k_max : 0);
   return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
+}
+
+// Summary-profile launches over a module order sorted by size (descending,
+// k_sorted[i] = size of d_order[i]): the modules above rg4_kernel_k_max() run
+// first on the scratch-Gram variants, the rest as one register-resident
+// (variant 5) launch, each launch with its own work queue and k_max.
+int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
+                    const std::vector<int32_t>& k_sorted, int64_t n_perm, hipStream_t st) {
+  const int n_mod = (int)k_sorted.size();
+  const int forced = profile_variant_env();
+  // The register-resident kernel is opt-in (NETREP_PROFILE_VARIANT=rg4): one
+  // wave per SIMD leaves its latency chains exposed and it measured 1.45x
+  // slower than packed4 on C3's <= 255-node modules (24.4 vs 16.7 ms per 256
+  // permutations; profiles/r02/profile_variants.txt).
+  int n_big = n_mod;
+  if (forced == 5) {
+    n_big = 0;
+    while (n_big < n_mod && k_sorted[n_big] > nr::rg4_kernel_k_max()) ++n_big;
+  }
+  struct Seg {
+    int first, count;
+    ProfilePlan plan;
+  } seg[2];
+  int ns = 0;
+  if (n_big > 0) seg[ns++] = {0, n_big, {}};
+  if (n_big < n_mod) seg[ns++] = {n_big, n_mod - n_big, {}};
+  for (int i = 0; i < ns; ++i) {
+    const int rc = plan_profile(ctx, (int64_t)seg[i].count * n_perm, k_sorted[seg[i].first], (int)pp.n_samples,
+                                seg[i].first == n_big, &seg[i].plan);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < ns; ++i) {  // scratch final after every plan
+    const ProfilePlan& plan = seg[i].plan;
+    const int k_max = k_sorted[seg[i].first];
+    pp.mod_order = d_order + seg[i].first;
+    pp.n_items = (int32_t)((int64_t)seg[i].count * n_perm);
+    pp.k_max = k_max;
+    pp.ld = gram_ld(k_max);
+    pp.m_max = profile_m_max(k_max);
+    pp.gram_doubles = plan.gram_doubles;
+    pp.scratch = ctx->d_scratch;
+    pp.scratch_stride = plan.stride;
+    pp.part_global = plan.variant == 4 ? 1 : 0;
+    NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
+    if (plan.variant == 5)
+      NR_HIP(ctx, nr::launch_profile_rg4(pp, plan.slots, st));
+    else
+      NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, st));
+  }
+  return NR_OK;
 }
 
 // Kernel timers: events on the kernel's own stream; collected (synchronised)
@@ -303,11 +373,6 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   // The network statistics are their own launch (module_net_kernel) ahead of
   // the summary-profile kernel; NETREP_CONCURRENT=1 puts them on the side
   // stream instead.
-  ProfilePlan plan;
-  if (data) {
-    rc = plan_profile(ctx, n_items, ctx->k_max, (int)ctx->n_samples, &plan);
-    if (rc) return rc;
-  }
   const bool fuse = false;
   const bool fork = data && !fuse && ctx->concurrent;
   hipStream_t net_stream = fork ? ctx->side : ctx->stream;
@@ -322,20 +387,13 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   }
 
   if (data) {
-    NR_HIP(ctx, hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream));
     nr::ProfileParams pp{};
     pp.data = ctx->d_data;
     pp.n_samples = ctx->n_samples;
     pp.src = src;
     pp.node_off = ctx->d_node_off;
     pp.disc_nc = ctx->d_disc_nc;
-    pp.mod_order = ctx->d_mod_order;
     pp.n_perm = (int32_t)n_perm;
-    pp.n_items = (int32_t)n_items;
-    pp.k_max = ctx->k_max;
-    pp.ld = gram_ld(ctx->k_max);
-    pp.gram_doubles = plan.gram_doubles;
-    pp.m_max = profile_m_max(ctx->k_max);
     pp.row_of = ctx->d_row_of;
     pp.n_rows = ctx->n_rows;
     pp.n_stat = n_stat;
@@ -343,16 +401,14 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.slot_cor_contrib = 4;
     pp.slot_avg_contrib = 6;
     pp.out = d_out;
-    pp.scratch = ctx->d_scratch;
-    pp.scratch_stride = plan.stride;
     pp.queue = ctx->d_counters;
     pp.diag = ctx->d_counters + 1;
     pp.stamps = ctx->d_stamps;
     pp.fuse_net = fuse ? 1 : 0;
-    pp.part_global = plan.variant == 4 ? 1 : 0;
     pp.net = np;
     timer_begin(ctx, 1, ctx->stream);
-    NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, ctx->stream));
+    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ctx->stream);
+    if (rc) return rc;
     timer_end(ctx, 1, n_items, ctx->stream);
   }
   if (fork) {
@@ -731,6 +787,8 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   if ((rc = upload(ctx, ctx->d_disc_nc, disc_contrib, disc_contrib ? (size_t)ctx->n_node_total : 0))) return rc;
   if ((rc = upload(ctx, ctx->d_cv_shift, shift.data(), shift.size()))) return rc;
   if ((rc = upload(ctx, ctx->d_mod_order, order.data(), order.size()))) return rc;
+  ctx->order_k_h.resize(n_present);
+  for (int i = 0; i < n_present; ++i) ctx->order_k_h[i] = (int32_t)(node_off[order[i] + 1] - node_off[order[i]]);
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->d_data && !ctx->d_disc_nc && n_present > 0)
     return fail(ctx, NR_ERR_INVALID, "dataset has data but disc_contrib is NULL");
@@ -868,30 +926,20 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
     np.avgw_out = d_aw;
     e = nr::launch_net(np, n_mod, ctx->stream);
     if (e == hipSuccess && ctx->d_data && (contribution || summary || coherence)) {
-      ProfilePlan plan;
-      if ((rc = plan_profile(ctx, n_mod, kmax, (int)S, &plan))) break;
-      e = hipMemsetAsync(ctx->d_counters, 0, sizeof(int), ctx->stream);
+      std::vector<int32_t> k_sorted(n_mod);
+      for (int i = 0; i < n_mod; ++i) k_sorted[i] = (int32_t)(node_off[order[i] + 1] - node_off[order[i]]);
       nr::ProfileParams pp{};
       pp.data = ctx->d_data;
       pp.n_samples = S;
       pp.src = src;
       pp.node_off = d_off;
-      pp.mod_order = d_order;
       pp.n_perm = 1;
-      pp.n_items = n_mod;
-      pp.k_max = kmax;
-      pp.ld = gram_ld(kmax);
-      pp.gram_doubles = plan.gram_doubles;
-      pp.m_max = profile_m_max(kmax);
       pp.sp_out = d_sp;
       pp.nc_out = d_nc;
       pp.coh_out = d_coh;
-      pp.scratch = ctx->d_scratch;
-      pp.scratch_stride = plan.stride;
       pp.queue = ctx->d_counters;
       pp.diag = ctx->d_counters + 1;
-      pp.part_global = plan.variant == 4 ? 1 : 0;
-      if (e == hipSuccess) e = nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, ctx->stream);
+      if ((rc = launch_profiles(ctx, pp, d_order, k_sorted, 1, ctx->stream))) break;
     }
     auto d2h = [&](double* h, const double* d, int64_t n) {
       if (e == hipSuccess && h && n > 0)

@@ -78,6 +78,11 @@ int reg_kernel_k_max();  // largest module of the register-resident scheme
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);
+// Register-resident 4-wave summary-profile kernel (kernels_rg4.hip).
+size_t rg4_kernel_lds();
+int rg4_kernel_k_max();
+constexpr int kRg4StepCap = 160;  // Lanczos steps (basis columns) per item
+hipError_t launch_profile_rg4(const ProfileParams& P, int n_slots, hipStream_t st);
 hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,
                              hipStream_t st);
 hipError_t launch_symmetry(const double2* a, int64_t n, int* asym, hipStream_t st);

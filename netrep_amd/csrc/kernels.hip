@@ -801,6 +801,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   int next_check = mcap < 16 ? mcap : 16;
   int prev_j = 0;  // lane 0 of wave 0 only
   double prev_r = 0.0;
+  double hint_theta = 0.0, hint_r = 0.0;  // previous check, every lane of wave 0 (warm start)
   const double sqrt_eps = 1.4901161193847656e-08;
   bool force_next = false;
   double anorm = 0.0;
@@ -848,8 +849,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     const bool last = (j + 1 == mcap);
     if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
       if (wave == 0) {
-        const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane);
+        const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane, hint_theta, hint_r);
         const double resid = tri_top_resid(alpha, beta, j + 1, theta, beta_j, ty, lane);
+        hint_theta = theta;
+        hint_r = resid;
         if (lane == 0) {
           const double tol = 5e-15 * fabs(theta);
           const bool conv = resid <= tol;

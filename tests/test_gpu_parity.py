@@ -334,7 +334,7 @@ def test_netprops_one_node_and_absent_modules(bundled):
     assert np.float64(got["ghost"]["avgWeight"]).view(np.uint64) == na
 
 
-@pytest.mark.parametrize("variant", ["reg", "packed4", "packed", "full"])
+@pytest.mark.parametrize("variant", ["rg4", "reg", "packed4", "packed", "full"])
 def test_profile_kernel_variants(variant, monkeypatch, bundled, bundled_expected):
     """Every summary-profile Gram scheme (NETREP_PROFILE_VARIANT) against the
     oracles: register-resident tiles, packed symmetric (4 and 8 waves), full

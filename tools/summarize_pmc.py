@@ -47,8 +47,20 @@ def main():
             d["hbm_bytes_corrected"] = d["FETCH_SIZE"] * 1024 * 2 + d.get("WRITE_SIZE", 0.0) * 1024
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1)
+        if "GRBM_GUI_ACTIVE" in d:
+            # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md,
+            # DVFS give-back): the kernel's own clock count is a 1/8 of it.
+            d["gui_active_cycles"] = d["GRBM_GUI_ACTIVE"] / 8
+            if "avg_ns" in d and d["avg_ns"] > 0:
+                d["effective_clock_ghz"] = d["gui_active_cycles"] / d["avg_ns"]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
-            d["mfma_busy_pct"] = 100 * d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] * 1024)
+            # busy cycles summed over the 1,024 SIMDs (256 CUs x 4)
+            d["mfma_busy_pct"] = 100 * d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8 * 1024)
+        if "SQ_INSTS_VALU_MFMA_MOPS_F64" in d:
+            # one MOPS unit = 512 executed f64 flops (16x16x4 f64: 2,048 flops = 4 units)
+            d["mfma_f64_flops_executed"] = 512 * d["SQ_INSTS_VALU_MFMA_MOPS_F64"]
+            if "avg_ns" in d and d["avg_ns"] > 0:
+                d["mfma_f64_tflops_executed"] = d["mfma_f64_flops_executed"] / d["avg_ns"] / 1e3
         if "SQ_WAVE_CYCLES" in d:
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 if c in d:
