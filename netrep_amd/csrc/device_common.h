@@ -498,6 +498,61 @@ __device__ __forceinline__ void profile_contrib(const ProfileParams& P, int k, i
   __syncthreads();
 }
 
+// Node contributions when Lanczos ran on the dual Gram (k > S): L.vv holds u
+// itself (unit norm, S entries). One pass over the module's data gives, per
+// node, x_c . u, the column sum and the sum of squares (one wave per node,
+// lanes over samples); then NC_c = cor(x_c, u) and the orientation exactly as
+// profile_contrib (src/netStats.cpp:242-247, 279). q, gv, colm are reused as
+// per-node scratch (sum of squares, x_c . u, column mean).
+template <int NW>
+__device__ __forceinline__ void profile_contrib_dual(const ProfileParams& P, int k, int m, const LzLds& L,
+                                                     const double* __restrict__ X, int S, double ones_g_ones) {
+  constexpr int BS = NW * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double Sd = (double)S;
+  const double* u = L.vv;
+  for (int c = wave; c < k; c += NW) {
+    const double* col = X + (int64_t)L.idx[c] * S;
+    double a = 0.0, b = 0.0, q = 0.0;
+    for (int s = lane; s < S; s += 64) {
+      const double x = col[s];
+      a = fma(x, u[s], a);
+      b += x;
+      q = fma(x, x, q);
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    q = wave_sum(q);
+    if (lane == 0) {
+      L.gv[c] = a;
+      L.colm[c] = b / Sd;
+      L.q[c] = q;
+    }
+  }
+  double a3[1] = {0.0};
+  for (int s = tid; s < S; s += BS) a3[0] += u[s];
+  block_sums<1, NW>(a3, L.red);  // its barriers also publish the per-node sums
+  const double ubar = a3[0] / Sd;
+  const double var_u = 1.0 - Sd * ubar * ubar;
+  double a4[2] = {0.0, 0.0};
+  for (int c = tid; c < k; c += BS) {
+    a4[0] += L.gv[c] - Sd * L.colm[c] * ubar;
+    a4[1] += L.colm[c];
+  }
+  block_sums<2, NW>(a4, L.red);
+  const double var_mo = ones_g_ones - Sd * a4[1] * a4[1];
+  const bool flip = (a4[0] < 0.0) && (var_mo > 0.0) && (var_u > 0.0);
+  const double sgn = flip ? -1.0 : 1.0;
+  for (int c = tid; c < k; c += BS) {
+    const double cov = L.gv[c] - Sd * L.colm[c] * ubar;
+    const double var_x = L.q[c] - Sd * L.colm[c] * L.colm[c];
+    L.w[c] = sgn * cov / (sqrt(var_x) * sqrt(var_u));
+  }
+  if (P.sp_out)
+    for (int s = tid; s < S; s += BS) P.sp_out[(int64_t)m * S + s] = sgn * u[s];
+  __syncthreads();
+}
+
 // svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235).
 template <int NW>
 __device__ __forceinline__ void profile_nonfinite(const ProfileParams& P, int k, int m, int S, const LzLds& L) {

@@ -191,7 +191,16 @@ struct ProfilePlan {
   int slots = 0;
   int per_cu = 1;
   int64_t gram_doubles = 0, stride = 0;
+  bool dual = false;  // S x S Gram for the modules with k > S
+  int k_gram = 0;     // side of the largest Gram (minus the ones column)
 };
+
+// The S x S (dual) Gram for modules larger than the sample count; on unless
+// NETREP_DUAL_GRAM=0 (A/B runs).
+bool dual_gram_enabled() {
+  const char* f = std::getenv("NETREP_DUAL_GRAM");
+  return !(f && f[0] == '0');
+}
 
 // NETREP_PROFILE_VARIANT (A/B runs): -1 when unset.
 int profile_variant_env() {
@@ -217,6 +226,9 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
   }
   const int forced = profile_variant_env();
   int variant = forced >= 0 && forced != 5 ? forced : 2;
+  // the dual (S x S) Gram of modules with k > S: the Gram side is min(k, S)
+  plan->dual = dual_gram_enabled() && variant != 3;
+  plan->k_gram = plan->dual ? std::min(k_max, n_samples) : k_max;
   if (variant == 3 && k_max > nr::reg_kernel_k_max()) variant = 2;
   if (variant != 0 && nr::profile_kernel_lds(k_max, m, n_samples, variant) > 160 * 1024) variant = 0;
   // Large modules: the per-wave matvec partials (4 x k doubles) move from LDS
@@ -237,10 +249,10 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
   if (variant == 3) {
     plan->gram_doubles = 0;  // the Gram lives in registers and LDS
   } else if (variant == 1 || variant == 2) {
-    const int64_t kc = k_max + 1;
+    const int64_t kc = plan->k_gram + 1;
     plan->gram_doubles = (kc * (kc + 1) / 2 + 1 + 31) / 32 * 32;  // packed triangle + zero pad
   } else {
-    const int64_t ld = gram_ld(k_max);
+    const int64_t ld = gram_ld(plan->k_gram);
     plan->gram_doubles = ld * ld;
   }
   plan->stride = plan->gram_doubles + (int64_t)k_max * m + (variant == 4 ? (int64_t)nr::kProfileWaves * k_max : 0);
@@ -282,8 +294,9 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.mod_order = d_order + seg[i].first;
     pp.n_items = (int32_t)((int64_t)seg[i].count * n_perm);
     pp.k_max = k_max;
-    pp.ld = gram_ld(k_max);
+    pp.ld = gram_ld(plan.variant == 5 ? k_max : plan.k_gram);
     pp.m_max = profile_m_max(k_max);
+    pp.dual = plan.dual ? 1 : 0;
     pp.gram_doubles = plan.gram_doubles;
     pp.scratch = ctx->d_scratch;
     pp.scratch_stride = plan.stride;

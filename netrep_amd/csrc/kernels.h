@@ -69,6 +69,7 @@ struct ProfileParams {
   unsigned long long* stamps;  // [8] per-phase shader cycles (diagnostics; NULL = off)
   int fuse_net;                // 1: each item also computes the network statistics (net)
   int part_global;             // 1: matvec partials (4 x k_max) at the end of the slot's scratch
+  int dual;                    // 1: modules with k > n_samples use the S x S Gram [X' 1]'[X' 1]
   NetParams net;
 };
 

@@ -601,6 +601,85 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
 }
 
 
+// Dual Gram for modules with more nodes than samples (k > S): H = [X' 1]' [X' 1]
+// over the k module nodes, i.e. X X' (S x S) bordered by the row sums X 1 and
+// k. Its top eigenvector is the summary profile u itself (the left singular
+// vector svd_econ returns, src/netStats.cpp:229-236), so Lanczos runs in
+// dimension S instead of k and the Gram costs 2 k S^2 flops instead of
+// 2 S k^2. Same super-tile / storage scheme as gram_mfma with the roles of
+// samples and nodes exchanged: operand columns are samples (16 consecutive
+// samples of one node per lane group: one 128-byte read), the contraction
+// runs over the nodes. Returns the per-lane part of |X 1|^2 (= 1'G1 of the
+// primal Gram; here the squared norm of H's ones column) and a non-finite flag.
+template <int NW = NR_WAVES, bool PACKED = false>
+__device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32_t* idx, int k,
+                               double* __restrict__ G, int ld, double& g1sum, int& bad) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int kc = S + 1;
+  const int T2 = (kc + 31) / 32;
+  const int nsup = T2 * (T2 + 1) / 2;
+  for (int t = wave; t < nsup; t += NW) {
+    int I2 = 0, rem = t;
+    while (rem >= T2 - I2) { rem -= T2 - I2; ++I2; }
+    const int J2 = I2 + rem;
+    const int cols[4] = {I2 * 32 + i16, I2 * 32 + 16 + i16, J2 * 32 + i16, J2 * 32 + 16 + i16};
+    nr_f64x4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+    auto load = [&](int c0, double (&v)[4][4]) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + q;
+        const double* col = c < k ? X + (int64_t)idx[c] * S : nullptr;
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+          v[o][q] = col ? (cols[o] < S ? col[cols[o]] : (cols[o] == S ? 1.0 : 0.0)) : 0.0;
+      }
+    };
+    double cur[4][4], nxt[4][4];
+    load(4 * kk, cur);
+    for (int c0 = 0; c0 < k; c0 += 16) {
+      if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[2][q], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[3][q], acc[1][1], 0, 0, 0);
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+    }
+    if (PACKED && t == 0 && lane == 0) G[pk_col(kc, kc)] = 0.0;  // zero pad read by packed_matvec
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = I2 * 32 + 16 * a + kk + 4 * r;
+          const int gj = J2 * 32 + 16 * b + i16;
+          const double val = acc[a][b][r];
+          if (PACKED) {
+            if (gi <= gj && gj < kc) G[pk_at(gj, gi, kc)] = val;
+          } else {
+            G[gi + (int64_t)gj * ld] = val;
+            G[gj + (int64_t)gi * ld] = val;
+          }
+          if (gj == S && gi < S) g1sum += val * val;  // |X 1|^2 from the row sums (X 1)_gi
+        }
+  }
+}
+
 // w = G x over the leading k x k block of the PACKED symmetric G (pk_at), NW
 // waves. Work units are (64-row block, 16-column group) pairs with columns
 // c <= last row of the block; lanes own rows. One coalesced read of each
@@ -943,25 +1022,35 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   int64_t p_local, off;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
-    // ---- Gram [X 1]^T [X 1] on the matrix cores ----
+    // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
+    const bool dual = P.dual && k > S;
+    const int n = dual ? S : k;  // Lanczos dimension
+    const int kc = n + 1;
     double g1[1] = {0.0};
     int bad = 0;
-    gram_mfma<NW, PACKED>(X, S, L.idx, k, G, ld, g1[0], bad);
-    const int kc = k + 1;
+    if (dual)
+      gram_mfma_dual<NW, PACKED>(X, S, L.idx, k, G, ld, g1[0], bad);
+    else
+      gram_mfma<NW, PACKED>(X, S, L.idx, k, G, ld, g1[0], bad);
     if (bad) atomicOr(&s_flags[1], 1);
     block_sums<1, NW>(g1, L.red);  // barriers also publish G to the whole workgroup
     NR_STAMP(1);  // Gram
     if (s_flags[1] == 0) {
-      for (int c = tid; c < k; c += BS)
-        L.colm[c] = (PACKED ? G[pk_at(k, c, kc)] : G[k + (int64_t)c * ld]) / Sd;
+      if (!dual)
+        for (int c = tid; c < k; c += BS)
+          L.colm[c] = (PACKED ? G[pk_at(k, c, kc)] : G[k + (int64_t)c * ld]) / Sd;
       auto mv = [&](const double* x, double* out, const double* y) -> double {
-        return PACKED ? packed_matvec<NW>(G, kc, k, x, out, part, upper, kmax, y, L.red)
-                      : matvec(G, ld, k, x, out, part, kmax, y, L.red);
+        return PACKED ? packed_matvec<NW>(G, kc, n, x, out, part, upper, kmax, y, L.red)
+                      : matvec(G, ld, n, x, out, part, kmax, y, L.red);
       };
-      lanczos_ritz<NW, PACKED>(P, k, L, s_flags, Q, mv, t_mark);
-      profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) {
-        return PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
-      });
+      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark);
+      if (dual) {
+        profile_contrib_dual<NW>(P, k, m, L, X, S, g1[0]);
+      } else {
+        profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) {
+          return PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
+        });
+      }
     } else {
       profile_nonfinite<NW>(P, k, m, S, L);
     }

@@ -1,0 +1,96 @@
+"""The S x S (dual) Gram for modules with more nodes than samples (k > S):
+Lanczos on H = [X' 1]'[X' 1] gives the summary profile u directly
+(src/netStats.cpp:229-236 takes U.col(0) of svd_econ); node contributions
+from one pass over the data. Checked against the C++ LAPACK restatement
+(dgesvd of the S x k block) on identical shuffles, against the primal k x k
+path (NETREP_DUAL_GRAM=0), in vector mode (NetProps' summary profiles) and
+through the non-finite (svd failure) path."""
+import numpy as np
+import pytest
+
+import netrep_amd as N
+from oracle import netrep_oracle as O
+
+from conftest import assert_stats_close
+from test_gpu_parity import _engine_from
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(sizes, n_samples, seed, n_nodes=3000):
+    from netrep_amd import synthetic as S
+    lay = S.make_layout(n_nodes, sizes, seed)
+    dx, dc, dn = S.numpy_dataset(lay, n_samples, seed + 1)
+    tx, tc, tn = S.numpy_dataset(lay, n_samples, seed + 2, preserve_all=False)
+    mi = O.ModuleIndex(lay.names, lay.labels, lay.names, lay.modules)
+    disc = O.intermediate_properties(O.scale(dx), dc, dn, mi.disc_idx(lay.names))
+    return lay, mi, disc, O.scale(tx), tc, tn
+
+
+def _cpp(mi, disc, txs, tc, tn, pis):
+    from oracle import ref_cpp
+    mods = mi.mods_present
+    node_off = np.concatenate([[0], np.cumsum([mi.test_idx[m].size for m in mods])])
+    return ref_cpp.permutation_procedure(
+        txs, tc, tn, len(mi.modules), [mi.modules.index(m) for m in mods], node_off,
+        np.concatenate([mi.test_idx[m] for m in mods]), np.concatenate([mi.null_pos[m] for m in mods]),
+        mi.null_idx, np.concatenate([disc["corr"][m] for m in mods]),
+        np.concatenate([disc["degree"][m] for m in mods]),
+        np.concatenate([disc["contribution"][m] for m in mods]), pis.shape[0], pi=pis, n_threads=8)
+
+
+@pytest.mark.parametrize("variant", [None, "full"])
+def test_dual_gram_vs_cpp_oracle(variant, monkeypatch):
+    """S = 40 with modules of 20-260 nodes: k > S (dual), k == S and k < S
+    (primal) in one launch; packed (default) and full Gram storage."""
+    if variant:
+        monkeypatch.setenv("NETREP_PROFILE_VARIANT", variant)
+    lay, mi, disc, txs, tc, tn = _case([260, 180, 64, 41, 40, 39, 20], 40, 5)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(10, 22, 99)
+    pis = N.prp_table(99, 10, 22, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (dual)")
+    assert_stats_close(nulls, exp, what="nulls (dual)")
+
+
+def test_dual_equals_primal(monkeypatch):
+    """The dual and the primal Gram give the same statistics (to rounding)."""
+    lay, mi, disc, txs, tc, tn = _case([200, 120, 70], 60, 9)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    a = eng.run(0, 16, 3)
+    monkeypatch.setenv("NETREP_DUAL_GRAM", "0")
+    eng2 = _engine_from(mi, disc, txs, tc, tn)
+    b = eng2.run(0, 16, 3)
+    assert_stats_close(a, b, what="dual vs primal")
+
+
+def test_dual_netprops_summary():
+    """Vector mode (NetProps, src/properties.cpp): summary profile, node
+    contributions and coherence of modules with k > S."""
+    from netrep_amd.api import RMatrix
+    lay, mi, disc, txs, tc, tn = _case([150, 90, 35], 30, 13, n_nodes=600)
+    names = lay.names
+    ma = dict(zip(names, lay.labels))
+    got = N.NetProps(RMatrix(txs, None, names), RMatrix(tn, names, names), ma, lay.modules)
+    module_nodes = {m: [n for n, l in ma.items() if l == m] for m in lay.modules}
+    exp = O.net_props(txs, tn, names, module_nodes, lay.modules)
+    for m in lay.modules:
+        for key in ("summary", "contribution"):
+            assert_stats_close(got[m][key], exp[m][key], what=f"{m}/{key}")
+        assert_stats_close([got[m]["coherence"]], [exp[m]["coherence"]], what=f"{m}/coherence")
+
+
+def test_dual_nonfinite_column_gives_na():
+    """A NaN data column inside a k > S module: svd_econ fails, the module's
+    summary-profile statistics are NA (src/netStats.cpp:229-235)."""
+    lay, mi, disc, txs, tc, tn = _case([90, 25], 20, 17, n_nodes=400)
+    txs = txs.copy()
+    m0 = mi.mods_present[0]
+    txs[:, mi.test_idx[m0][3]] = np.nan
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    obs = eng.observed()
+    _, exp = O.permutation_procedure(disc, txs, tc, tn, mi, np.zeros((0, mi.null_idx.size), int))
+    assert_stats_close(obs, exp, what="observed with NaN column (dual)")
+    row = mi.mods_present.index(m0)
+    assert not np.isfinite(obs[row, [1, 4, 6]]).any()
