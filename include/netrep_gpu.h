@@ -30,14 +30,15 @@ extern "C" {
 #define NR_ERR_HIP 1          /* HIP runtime / launch failure */
 #define NR_ERR_INVALID 2      /* bad argument, shape or missing prerequisite */
 #define NR_ERR_OOM 3          /* device allocation failed */
-#define NR_ERR_UNSUPPORTED 4  /* size beyond an engine limit (e.g. module > NR_MAX_MODULE_NODES) */
+#define NR_ERR_UNSUPPORTED 4  /* size beyond an engine limit: a module of more nodes than the
+                                 summary-profile kernel's LDS vectors hold (~2,500) in a dataset
+                                 of more samples than that (modules of any size are accepted
+                                 otherwise, as src/netStats.cpp:217-280) */
 #define NR_ERR_CANCELLED 5    /* nr_cancel() was called during a run */
 #define NR_ERR_NONFINITE 6    /* CheckFinite failure (src/checkFinite.cpp:25-27) */
 
 #define NR_HOST 0
 #define NR_DEVICE 1
-
-#define NR_MAX_MODULE_NODES 2048
 
 /* Statistic slots in the nulls cube (src/permutations.cpp:95-101, :174-177). */
 #define NR_NSTAT_DATA 7

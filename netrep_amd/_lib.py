@@ -22,7 +22,6 @@ NR_ERR_CANCELLED = 5
 NR_ERR_NONFINITE = 6
 NR_HOST = 0
 NR_DEVICE = 1
-NR_MAX_MODULE_NODES = 2048
 
 
 class NetRepError(RuntimeError):

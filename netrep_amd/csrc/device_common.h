@@ -618,7 +618,8 @@ __device__ __forceinline__ void profile_stats(const ProfileParams& P, int k, int
 // offset, k) and its index set in L.idx. Returns false when drained.
 template <int NW>
 __device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L, int* flags, int& m,
-                                          int64_t& p_local, int64_t& off, int& k) {
+                                          int64_t& p_local, int64_t& off, int& k, int kvec = 1 << 30,
+                                          uint32_t* gidx = nullptr, uint32_t** idx_used = nullptr) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x;
   if (tid == 0) flags[0] = atomicAdd(P.queue, 1);
@@ -633,7 +634,10 @@ __device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L
   k = (int)(P.node_off[m + 1] - off);
   nr_prp_key key;
   if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
-  for (int c = tid; c < k; c += BS) L.idx[c] = node_index(P.src, key, p_local, off + c);
+  // modules longer than the LDS vectors: index set in the slot's scratch
+  uint32_t* dst = (k <= kvec || !gidx) ? L.idx : gidx;
+  if (idx_used) *idx_used = dst;
+  for (int c = tid; c < k; c += BS) dst[c] = node_index(P.src, key, p_local, off + c);
   if (tid == 0) flags[1] = 0;
   __syncthreads();
   return true;

@@ -84,6 +84,8 @@ struct nr_ctx {
   size_t pi_cap = 0;
   double* d_scratch = nullptr;
   size_t scratch_cap = 0;
+  double* d_net_scratch = nullptr;  // per-workgroup node arrays of modules too large for LDS
+  size_t net_scratch_cap = 0;
   int* d_counters = nullptr;  // [0] queue head, [1..4] lanczos diagnostics, [5] flag
   int64_t batch = 0;          // 0 = automatic
 
@@ -193,6 +195,10 @@ struct ProfilePlan {
   int64_t gram_doubles = 0, stride = 0;
   bool dual = false;  // S x S Gram for the modules with k > S
   int k_gram = 0;     // side of the largest Gram (minus the ones column)
+  int m = 0;          // Lanczos basis columns
+  int kvec = 0;       // LDS vector length
+  bool big = false;   // modules beyond kvec (per-node arrays in scratch)
+  int64_t basis_doubles = 0;
 };
 
 // The S x S (dual) Gram for modules larger than the sample count; on unless
@@ -215,7 +221,6 @@ int profile_variant_env() {
 int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg4, ProfilePlan* plan) {
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-  const int m = profile_m_max(k_max);
   if (rg4) {
     plan->variant = 5;
     plan->per_cu = 1;
@@ -226,15 +231,32 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
   }
   const int forced = profile_variant_env();
   int variant = forced >= 0 && forced != 5 ? forced : 2;
-  // the dual (S x S) Gram of modules with k > S: the Gram side is min(k, S)
+  // the dual (S x S) Gram of modules with k > S: the Gram side is min(k, S),
+  // and so is every Lanczos dimension (basis columns of that length)
   plan->dual = dual_gram_enabled() && variant != 3;
   plan->k_gram = plan->dual ? std::min(k_max, n_samples) : k_max;
+  const int mg = profile_m_max(plan->k_gram);
+  plan->m = mg;
+  int kvec = k_max;
   if (variant == 3 && k_max > nr::reg_kernel_k_max()) variant = 2;
-  if (variant != 0 && nr::profile_kernel_lds(k_max, m, n_samples, variant) > 160 * 1024) variant = 0;
+  if (variant != 0 && nr::profile_kernel_lds(kvec, mg, n_samples, variant) > 160 * 1024) variant = 0;
   // Large modules: the per-wave matvec partials (4 x k doubles) move from LDS
   // to the slot's scratch, which leaves LDS for the six Lanczos vectors only.
-  if (variant == 0 && nr::profile_kernel_lds(k_max, m, n_samples, 0) > 160 * 1024) variant = 4;
-  const size_t lds = nr::profile_kernel_lds(k_max, m, n_samples, variant);
+  if (variant == 0 && nr::profile_kernel_lds(kvec, mg, n_samples, 0) > 160 * 1024) variant = 4;
+  // Modules beyond even those vectors (any k up to N, as src/netStats.cpp:
+  // 217-280): Lanczos runs on the dual Gram (dimension S <= kvec) and their
+  // per-node arrays live in the slot's scratch.
+  plan->big = false;
+  if (variant == 4 && nr::profile_kernel_lds(kvec, mg, n_samples, 4) > 160 * 1024) {
+    kvec = nr::profile_kvec_max(mg);
+    if (!plan->dual || n_samples > kvec)
+      return fail(ctx, NR_ERR_UNSUPPORTED,
+                  "module of more than " + std::to_string(kvec) + " nodes needs the dual Gram and at most " +
+                      std::to_string(kvec) + " samples");
+    plan->big = true;
+  }
+  plan->kvec = kvec;
+  const size_t lds = nr::profile_kernel_lds(kvec, mg, n_samples, variant);
   if (lds > 160 * 1024)
     return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
   int want = variant == 1 ? 2 : 3;
@@ -255,7 +277,10 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
     const int64_t ld = gram_ld(plan->k_gram);
     plan->gram_doubles = ld * ld;
   }
-  plan->stride = plan->gram_doubles + (int64_t)k_max * m + (variant == 4 ? (int64_t)nr::kProfileWaves * k_max : 0);
+  plan->basis_doubles = (int64_t)plan->k_gram * mg;
+  plan->stride = plan->gram_doubles + plan->basis_doubles +
+                 (variant == 4 ? (int64_t)nr::kProfileWaves * kvec : 0) +
+                 (plan->big ? 5 * (int64_t)k_max : 0);  // x.u, means, squares, contributions, index set
   return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
 }
 
@@ -295,8 +320,10 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.n_items = (int32_t)((int64_t)seg[i].count * n_perm);
     pp.k_max = k_max;
     pp.ld = gram_ld(plan.variant == 5 ? k_max : plan.k_gram);
-    pp.m_max = profile_m_max(k_max);
+    pp.m_max = plan.variant == 5 ? profile_m_max(k_max) : plan.m;
     pp.dual = plan.dual ? 1 : 0;
+    pp.kvec = plan.variant == 5 ? 0 : plan.kvec;
+    pp.basis_doubles = plan.basis_doubles;
     pp.gram_doubles = plan.gram_doubles;
     pp.scratch = ctx->d_scratch;
     pp.scratch_stride = plan.stride;
@@ -350,6 +377,44 @@ nr::IndexSource make_source(const nr_ctx* ctx, int mode, uint64_t seed, int64_t 
   return s;
 }
 
+// Network kernel scratch for modules whose per-node arrays exceed LDS: a
+// persistent grid of two workgroups per CU, each with its own slot.
+int prepare_net(nr_ctx* ctx, nr::NetParams& np, int64_t n_items) {
+  if (!nr::net_kernel_big(np.k_max)) return NR_OK;
+  int dev_cu = 256;
+  (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+  const int64_t slots = std::max<int64_t>(1, std::min<int64_t>(n_items, 2 * (int64_t)dev_cu));
+  const int64_t per = (int64_t)(nr::net_big_slot_bytes(np.k_max) / sizeof(double));
+  const int rc = ensure(ctx, ctx->d_net_scratch, ctx->net_scratch_cap, (size_t)(per * slots));
+  if (rc) return rc;
+  np.big_scratch = ctx->d_net_scratch;
+  np.big_stride = per;
+  np.big_slots = (int32_t)slots;
+  return NR_OK;
+}
+
+// Network-statistics launches over the size-sorted module order: modules
+// whose per-node arrays do not fit LDS first (global-scratch workgroups), the
+// rest in the ordinary one-workgroup-per-item launch with their own k_max.
+int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std::vector<int32_t>& k_sorted,
+                int64_t n_perm, hipStream_t st) {
+  const int n_mod = (int)k_sorted.size();
+  int n_big = 0;
+  while (n_big < n_mod && nr::net_kernel_big(k_sorted[n_big])) ++n_big;
+  const int first[2] = {0, n_big}, count[2] = {n_big, n_mod - n_big};
+  for (int i = 0; i < 2; ++i) {
+    if (count[i] == 0) continue;
+    nr::NetParams q = np;
+    q.mod_order = d_order + first[i];
+    q.k_max = k_sorted[first[i]];
+    const int64_t items = (int64_t)count[i] * n_perm;
+    const int rc = prepare_net(ctx, q, items);
+    if (rc) return rc;
+    NR_HIP(ctx, nr::launch_net(q, items, st));
+  }
+  return NR_OK;
+}
+
 // Launch the statistics kernels for n_perm permutations (or the observed /
 // direct sets when src.mode == NR_IDX_DIRECT, n_perm == 1) into d_out.
 int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double* d_out) {
@@ -395,7 +460,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   }
   if (!fuse) {
     timer_begin(ctx, 0, net_stream);
-    NR_HIP(ctx, nr::launch_net(np, n_items, net_stream));
+    if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ctx->order_k_h, n_perm, net_stream))) return rc;
     timer_end(ctx, 0, n_items, net_stream);
   }
 
@@ -626,6 +691,7 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   dfree(ctx->d_out);
   dfree(ctx->d_pi);
   dfree(ctx->d_scratch);
+  dfree(ctx->d_net_scratch);
   dfree(ctx->d_counters);
   dfree(ctx->d_stamps);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
@@ -758,8 +824,6 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   for (int m = 0; m < n_present; ++m) {
     const int64_t k = node_off[m + 1] - node_off[m];
     if (k <= 0) return fail(ctx, NR_ERR_INVALID, "present module with no nodes");
-    if (k > NR_MAX_MODULE_NODES)
-      return fail(ctx, NR_ERR_UNSUPPORTED, "module larger than NR_MAX_MODULE_NODES nodes");
     if (row_of[m] < 0 || row_of[m] >= n_rows) return fail(ctx, NR_ERR_INVALID, "row_of out of range");
     kmax = std::max<int32_t>(kmax, (int32_t)k);
     ctx->cv_off_h[m + 1] = ctx->cv_off_h[m] + k * (k - 1) / 2;
@@ -889,7 +953,6 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
   for (int m = 0; m < n_mod; ++m) {
     const int64_t k = node_off[m + 1] - node_off[m];
     if (k <= 0) return fail(ctx, NR_ERR_INVALID, "module with no nodes");
-    if (k > NR_MAX_MODULE_NODES) return fail(ctx, NR_ERR_UNSUPPORTED, "module larger than NR_MAX_MODULE_NODES");
     kmax = std::max<int32_t>(kmax, (int32_t)k);
     cv[m + 1] = cv[m] + k * (k - 1) / 2;
   }
@@ -937,10 +1000,11 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
     np.cv_out = d_cvo;
     np.wd_out = d_wd;
     np.avgw_out = d_aw;
-    e = nr::launch_net(np, n_mod, ctx->stream);
-    if (e == hipSuccess && ctx->d_data && (contribution || summary || coherence)) {
-      std::vector<int32_t> k_sorted(n_mod);
-      for (int i = 0; i < n_mod; ++i) k_sorted[i] = (int32_t)(node_off[order[i] + 1] - node_off[order[i]]);
+    std::vector<int32_t> k_sorted(n_mod);
+    for (int i = 0; i < n_mod; ++i) k_sorted[i] = (int32_t)(node_off[order[i] + 1] - node_off[order[i]]);
+    if ((rc = launch_nets(ctx, np, d_order, k_sorted, 1, ctx->stream))) break;
+    e = hipSuccess;
+    if (ctx->d_data && (contribution || summary || coherence)) {
       nr::ProfileParams pp{};
       pp.data = ctx->d_data;
       pp.n_samples = S;

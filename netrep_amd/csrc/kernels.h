@@ -41,6 +41,12 @@ struct NetParams {
   double* cv_out;              // vector outputs (NULL unless vector mode)
   double* wd_out;
   double* avgw_out;            // [n_mod] average edge weight (vector mode)
+  int64_t n_items;             // items of this launch (set by launch_net)
+  // Modules too large for the per-node arrays in LDS: a persistent grid of
+  // big_slots workgroups, each with big_stride doubles of global scratch
+  double* big_scratch;
+  int64_t big_stride;
+  int32_t big_slots;
 };
 
 struct ProfileParams {
@@ -70,11 +76,17 @@ struct ProfileParams {
   int fuse_net;                // 1: each item also computes the network statistics (net)
   int part_global;             // 1: matvec partials (4 x k_max) at the end of the slot's scratch
   int dual;                    // 1: modules with k > n_samples use the S x S Gram [X' 1]'[X' 1]
+  int32_t kvec;                // LDS vector length (0: k_max); larger (dual) modules keep their
+                               // per-node arrays in the slot's scratch
+  int64_t basis_doubles;       // Lanczos basis doubles per slot (behind the Gram)
   NetParams net;
 };
 
 size_t net_kernel_lds(int k_max);
+bool net_kernel_big(int k_max);        // per-node arrays in global scratch
+size_t net_big_slot_bytes(int k_max);  // global scratch per workgroup in that mode
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant);
+int profile_kvec_max(int m_max);  // longest LDS vectors of the large-module layout (variant 4)
 int reg_kernel_k_max();  // largest module of the register-resident scheme
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,

@@ -95,6 +95,15 @@ __device__ __forceinline__ NetLds carve_net_lds(unsigned char* smem, int kmax) {
   return L;
 }
 
+// The same layout in a workgroup's global scratch slot (modules too large for
+// LDS); only the reduction scratch stays in LDS.
+template <int NW>
+__device__ __forceinline__ NetLds carve_net_mem(unsigned char* smem, double* slot, int kmax) {
+  NetLds L = carve_net_lds<NW>(reinterpret_cast<unsigned char*>(slot) - sizeof(double) * 8 * NW, kmax);
+  L.red = reinterpret_cast<double*>(smem);
+  return L;
+}
+
 size_t net_lds_bytes(int nw, int kmax) {
   return sizeof(double) * (8 * (size_t)nw + (size_t)(nw + 2) * kmax) + sizeof(unsigned long long) * 3 * (size_t)kmax +
          sizeof(int) * 3 * (size_t)kmax;
@@ -342,23 +351,29 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
 }
 
 // Kernel 1: module network statistics. One workgroup of NW waves per item
-// (NW = 2 for modules too large for four waves' LDS copies).
-template <int NW>
+// (NW = 2 for modules too large for four waves' LDS copies). BIG: modules too
+// large for LDS at all -- a persistent grid whose workgroups keep the per-node
+// arrays in their global scratch slot (L2-resident; the atomics go to L2) and
+// loop over the items.
+template <int NW, bool BIG>
 __global__ void __launch_bounds__(NW * 64)
 module_net_kernel(NetParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const NetLds L = carve_net_lds<NW>(smem, P.k_max);
-  const int64_t item = blockIdx.x;
-  const int64_t mslot = item / P.n_perm;
-  const int64_t p_local = item - mslot * P.n_perm;
-  const int m = P.mod_order[mslot];
-  const int64_t off = P.node_off[m];
-  const int64_t k = P.node_off[m + 1] - off;
-  nr_prp_key key;
-  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
-  for (int64_t c = threadIdx.x; c < k; c += NW * 64) L.idx[c] = node_index(P.src, key, p_local, off + c);
-  __syncthreads();
-  net_item<NW>(P, m, p_local, off, k, L);
+  const NetLds L = BIG ? carve_net_mem<NW>(smem, P.big_scratch + (int64_t)blockIdx.x * P.big_stride, P.k_max)
+                       : carve_net_lds<NW>(smem, P.k_max);
+  const int64_t step = BIG ? (int64_t)gridDim.x : P.n_items;
+  for (int64_t item = blockIdx.x; item < P.n_items; item += step) {
+    const int64_t mslot = item / P.n_perm;
+    const int64_t p_local = item - mslot * P.n_perm;
+    const int m = P.mod_order[mslot];
+    const int64_t off = P.node_off[m];
+    const int64_t k = P.node_off[m + 1] - off;
+    nr_prp_key key;
+    if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
+    for (int64_t c = threadIdx.x; c < k; c += NW * 64) L.idx[c] = node_index(P.src, key, p_local, off + c);
+    __syncthreads();
+    net_item<NW>(P, m, p_local, off, k, L);
+  }
 }
 
 
@@ -1000,7 +1015,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_flags[8];
-  const int kmax = KB > 0 ? KB : P.k_max;
+  const int kmax = KB > 0 ? KB : (P.kvec > 0 ? P.kvec : P.k_max);  // LDS vector length
   const int mmax = KB > 0 ? (KB < 160 ? KB : 160) : P.m_max;
   const int S = (int)P.n_samples;
   double* part;
@@ -1013,15 +1028,29 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;  // Gram
   const int ld = P.ld;
   double* Q = G + P.gram_doubles;                                  // Lanczos basis
-  if (pglob) part = Q + (int64_t)kmax * mmax;
+  if (pglob) part = Q + P.basis_doubles;
   double* upper = part + NW * kmax;  // packed only
+  // modules of more than kmax nodes (dual by construction, engine.hip
+  // plan_profile): x_c.u, column means, sums of squares, contributions and the
+  // index set in the slot's scratch
+  double* gnode = Q + P.basis_doubles + (pglob ? (int64_t)NW * kmax : 0);
   const double* __restrict__ X = P.data;
   const double Sd = (double)S;
 
   int m, k;
   int64_t p_local, off;
-  while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
+  uint32_t* idx_p = L.idx;
+  while (next_item<NW>(P, L, s_flags, m, p_local, off, k, kmax,
+                       reinterpret_cast<uint32_t*>(gnode + 4 * (int64_t)P.k_max), &idx_p)) {
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
+    LzLds Li = L;  // this item's view: per-node arrays in scratch when k > kmax
+    Li.idx = idx_p;
+    if (k > kmax) {
+      Li.gv = gnode;
+      Li.colm = gnode + P.k_max;
+      Li.q = gnode + 2 * (int64_t)P.k_max;
+      Li.w = gnode + 3 * (int64_t)P.k_max;
+    }
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     const bool dual = P.dual && k > S;
     const int n = dual ? S : k;  // Lanczos dimension
@@ -1029,7 +1058,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     double g1[1] = {0.0};
     int bad = 0;
     if (dual)
-      gram_mfma_dual<NW, PACKED>(X, S, L.idx, k, G, ld, g1[0], bad);
+      gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, ld, g1[0], bad);
     else
       gram_mfma<NW, PACKED>(X, S, L.idx, k, G, ld, g1[0], bad);
     if (bad) atomicOr(&s_flags[1], 1);
@@ -1045,16 +1074,16 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       };
       lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark);
       if (dual) {
-        profile_contrib_dual<NW>(P, k, m, L, X, S, g1[0]);
+        profile_contrib_dual<NW>(P, k, m, Li, X, S, g1[0]);
       } else {
         profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) {
           return PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
         });
       }
     } else {
-      profile_nonfinite<NW>(P, k, m, S, L);
+      profile_nonfinite<NW>(P, k, m, S, Li);
     }
-    profile_stats<NW>(P, k, m, off, p_local, L);
+    profile_stats<NW>(P, k, m, off, p_local, Li);
     NR_STAMP(5);  // Ritz vector, contributions, statistics
   }
 }
@@ -1554,7 +1583,13 @@ __global__ void export_indices_kernel(IndexSource src, int64_t n_nodes_total, in
 // fit the LDS (modules of more than ~1,900 nodes): then two.
 int net_kernel_waves(int k_max) { return net_lds_bytes(4, k_max) <= 160 * 1024 ? 4 : 2; }
 
-size_t net_kernel_lds(int k_max) { return net_lds_bytes(net_kernel_waves(k_max), k_max); }
+bool net_kernel_big(int k_max) { return net_lds_bytes(2, k_max) > 160 * 1024; }
+
+size_t net_kernel_lds(int k_max) {
+  return net_kernel_big(k_max) ? sizeof(double) * 8 * 4 : net_lds_bytes(net_kernel_waves(k_max), k_max);
+}
+
+size_t net_big_slot_bytes(int k_max) { return (net_lds_bytes(4, k_max) + 255) / 256 * 256; }
 
 // Compile-time module-size bucket of the packed kernel (0 = runtime layout).
 int packed_bucket(int k_max) { return k_max <= 320 ? 320 : 0; }
@@ -1570,6 +1605,12 @@ int reg_kernel_k_max() { return RG_KP - 1; }
 
 // variant: 0 full Gram (4 waves), 1 packed (8 waves), 2 packed (4 waves),
 // 3 register-resident (8 waves, one workgroup per CU)
+int profile_kvec_max(int m_max) {
+  const size_t fixed = sizeof(double) * (8 * NR_WAVES + 12 * (size_t)m_max + 3);
+  const size_t per = 6 * sizeof(double) + sizeof(uint32_t);
+  return (int)((160 * 1024 - fixed) / per) / 16 * 16;
+}
+
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
   (void)n_samples;
   if (variant == 3) return reg_kernel_lds(m_max);
@@ -1585,19 +1626,26 @@ size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
          sizeof(uint32_t) * k_max;
 }
 
-hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st) {
+hipError_t launch_net(const NetParams& P0, int64_t n_items, hipStream_t st) {
+  NetParams P = P0;
+  P.n_items = n_items;
+  if (n_items <= 0) return hipSuccess;
   const size_t lds = net_kernel_lds(P.k_max);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (net_kernel_waves(P.k_max) == 4)
-    hipLaunchKernelGGL(module_net_kernel<4>, dim3((unsigned)n_items), dim3(256), lds, st, P);
-  else
-    hipLaunchKernelGGL(module_net_kernel<2>, dim3((unsigned)n_items), dim3(128), lds, st, P);
+  if (net_kernel_big(P.k_max)) {
+    if (!P.big_scratch || P.big_slots <= 0) return hipErrorInvalidValue;
+    const unsigned g = (unsigned)(n_items < P.big_slots ? n_items : P.big_slots);
+    hipLaunchKernelGGL((module_net_kernel<4, true>), dim3(g), dim3(256), lds, st, P);
+  } else if (net_kernel_waves(P.k_max) == 4) {
+    hipLaunchKernelGGL((module_net_kernel<4, false>), dim3((unsigned)n_items), dim3(256), lds, st, P);
+  } else {
+    hipLaunchKernelGGL((module_net_kernel<2, false>), dim3((unsigned)n_items), dim3(128), lds, st, P);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st) {
-  const size_t lds = profile_kernel_lds(P.k_max, P.m_max, (int)P.n_samples, variant);
+  const size_t lds = profile_kernel_lds(P.kvec > 0 ? P.kvec : P.k_max, P.m_max, (int)P.n_samples, variant);
   const dim3 g((unsigned)n_slots), b(512), b4(NR_BS);
   const bool b320 = packed_bucket(P.k_max) == 320;
   const bool packed = variant == 1;

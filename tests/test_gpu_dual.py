@@ -94,3 +94,35 @@ def test_dual_nonfinite_column_gives_na():
     assert_stats_close(obs, exp, what="observed with NaN column (dual)")
     row = mi.mods_present.index(m0)
     assert not np.isfinite(obs[row, [1, 4, 6]]).any()
+
+
+def test_modules_beyond_lds_vs_cpp_oracle():
+    """Modules of 2,500 and 3,000 nodes at S = 1,000 (no module cap, as
+    src/netStats.cpp:217-280): the 3,000-node module exceeds the LDS vectors
+    (its per-node arrays go to the slot's scratch) and both exceed the network
+    kernel's LDS (global-scratch workgroups). Against the C++ LAPACK
+    restatement on identical shuffles."""
+    lay, mi, disc, txs, tc, tn = _case([3000, 2500, 400], 1000, 21, n_nodes=7000)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(5, 7, 123)
+    pis = N.prp_table(123, 5, 7, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (k up to 3,000)")
+    assert_stats_close(nulls, exp, what="nulls (k up to 3,000)")
+
+
+def test_netprops_beyond_lds():
+    """Vector mode for a 2,600-node module at S = 300: weighted degree and
+    summary profile / contributions of a module beyond both kernels' LDS."""
+    from netrep_amd.api import RMatrix
+    lay, mi, disc, txs, tc, tn = _case([2600, 50], 300, 23, n_nodes=4000)
+    names = lay.names
+    ma = dict(zip(names, lay.labels))
+    got = N.NetProps(RMatrix(txs, None, names), RMatrix(tn, names, names), ma, lay.modules)
+    module_nodes = {m: [n for n, l in ma.items() if l == m] for m in lay.modules}
+    exp = O.net_props(txs, tn, names, module_nodes, lay.modules)
+    for m in lay.modules:
+        for key in ("summary", "contribution", "degree"):
+            assert_stats_close(got[m][key], exp[m][key], what=f"{m}/{key}")
+        assert_stats_close([got[m]["coherence"]], [exp[m]["coherence"]], what=f"{m}/coherence")
+        assert_stats_close([got[m]["avgWeight"]], [exp[m]["avgWeight"]], what=f"{m}/avgWeight")
