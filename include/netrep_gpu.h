@@ -232,6 +232,21 @@ int netrep_PermutationProcedure(
     int32_t n_cores, const char* null_hypothesis, int32_t verbose,
     uint64_t seed, const uint32_t* pi, double* nulls_out, double* observed_out);
 
+/* Pipelining modulePreservation's loop over test datasets
+ * (R/modulePreservation.R:553-620, one PermutationProcedure call per test
+ * dataset): starts uploading the NEXT test dataset's matrices to GPU 0 in the
+ * background (pinned, double-buffered chunks on the copy engine) and returns
+ * at once: prefetch dataset t+1, then call netrep_PermutationProcedure on
+ * dataset t, and the host->HBM copy of t+1 overlaps t's permutations. The
+ * netrep_PermutationProcedure call naming the same three pointers and sizes
+ * adopts the uploaded dataset instead of copying it again. At most two
+ * prefetches are pending (the oldest is dropped beyond that); the arrays must
+ * stay alive and unchanged until adopted or discarded. No reference
+ * counterpart (the reference loads one test dataset at a time into RAM). */
+int netrep_PrefetchTestDataset(const double* t_data, const double* t_corr, const double* t_net,
+                               int64_t n_samples, int64_t n_nodes);
+void netrep_DiscardPrefetch(void);
+
 /* IntermediateProperties[NoData] (src/discProps.cpp:44-48, :171-175).
  * Outputs per module in `modules` order, concatenated; lengths written to
  * *_len (0 for modules absent from the test node list). Buffers must hold

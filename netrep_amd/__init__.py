@@ -10,10 +10,12 @@ The compute path is the HIP library ``netrep_amd/_lib/libnetrep_amd.so``.
 from ._lib import NetRepError, load  # noqa: F401
 from .api import (CheckFinite, IntermediateProperties, IntermediatePropertiesNoData,  # noqa: F401
                   NetProps, NetPropsNoData, PermutationProcedure, PermutationProcedureNoData,
-                  RMatrix, Scale, STATNAMES, STATNAMES_NODATA, set_interrupt_hook)
+                  PrefetchTestDataset, DiscardPrefetch, RMatrix, Scale, STATNAMES, STATNAMES_NODATA,
+                  set_interrupt_hook)
 from .engine import Engine, device_count, prp_table  # noqa: F401
 
 __all__ = ["CheckFinite", "IntermediateProperties", "IntermediatePropertiesNoData", "NetProps",
            "NetPropsNoData", "PermutationProcedure", "PermutationProcedureNoData", "RMatrix",
            "Scale", "Engine", "NetRepError", "device_count", "prp_table", "STATNAMES",
-           "STATNAMES_NODATA", "set_interrupt_hook"]
+           "STATNAMES_NODATA", "set_interrupt_hook", "PrefetchTestDataset",
+           "DiscardPrefetch"]

@@ -93,6 +93,8 @@ SIGNATURES = {
     "netrep_CheckFinite": (_int, [_dp, _i64, _i64]),
     "netrep_last_error": (C.c_char_p, []),
     "netrep_set_interrupt_hook": (None, [C.c_void_p, C.c_void_p]),
+    "netrep_PrefetchTestDataset": (_int, [_dp, _dp, _dp, _i64, _i64]),
+    "netrep_DiscardPrefetch": (None, []),
 }
 
 _lib = None

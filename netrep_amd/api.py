@@ -174,6 +174,39 @@ def set_interrupt_hook(fn) -> None:
     lib.netrep_set_interrupt_hook(C.cast(cb, C.c_void_p), None)
 
 
+# Datasets handed to netrep_PrefetchTestDataset: their column-major arrays
+# stay referenced here until the PermutationProcedure call that adopts them
+# (at most two pending, as in the library).
+_prefetched = []
+
+
+def _prefetch_key(t_data, t_corr, t_net):
+    return (id(t_data.values) if t_data is not None else None, id(t_corr.values), id(t_net.values))
+
+
+def PrefetchTestDataset(tData: Optional[RMatrix], tCorr: RMatrix, tNet: RMatrix) -> None:
+    """Start uploading a later test dataset to the GPU in the background
+    (netrep_PrefetchTestDataset), so that its host->HBM copy overlaps the
+    permutations of the current one -- modulePreservation's loop over test
+    datasets (R/modulePreservation.R:553-620): prefetch dataset t+1, then run
+    dataset t. The PermutationProcedure call on these same matrices adopts
+    the upload."""
+    lib = L.load()
+    corr, net = tCorr.f, tNet.f
+    data = tData.f if tData is not None else None
+    s = data.shape[0] if data is not None else 0
+    rc = lib.netrep_PrefetchTestDataset(_dptr(data), _dptr(corr), _dptr(net), s, corr.shape[0])
+    L.check_api(rc)
+    _prefetched.append((_prefetch_key(tData, tCorr, tNet), (data, corr, net), (tData, tCorr, tNet)))
+    del _prefetched[:-2]
+
+
+def DiscardPrefetch() -> None:
+    """Drop every pending PrefetchTestDataset upload (netrep_DiscardPrefetch)."""
+    L.load().netrep_DiscardPrefetch()
+    _prefetched.clear()
+
+
 def _permutation(disc_props, t_data, t_corr, t_net, module_assignments, modules, n_perm, n_cores,
                  null_hypothesis, verbose, seed, pi):
     lib = L.load()
@@ -182,8 +215,14 @@ def _permutation(disc_props, t_data, t_corr, t_net, module_assignments, modules,
     with_data = t_data is not None
     t_names = list(t_net.colnames)
     n = len(t_names)
-    corr, net = t_corr.f, t_net.f
-    data = t_data.f if with_data else None
+    key = _prefetch_key(t_data, t_corr, t_net)
+    pre = next((p for p in _prefetched if p[0] == key), None)
+    if pre is not None:
+        _prefetched.remove(pre)
+        data, corr, net = pre[1]   # the very arrays the upload read (same pointers)
+    else:
+        corr, net = t_corr.f, t_net.f
+        data = t_data.f if with_data else None
     s = data.shape[0] if with_data else 0
     nm_ = len(modules)
     keep = []

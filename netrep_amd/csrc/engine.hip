@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -708,6 +709,67 @@ const char* nr_last_error(const nr_ctx* ctx) {
   return ctx ? ctx->err.c_str() : g_create_error.c_str();
 }
 
+// Copy n doubles with up to 8 host threads (pageable -> pinned staging).
+static void parallel_copy(double* dst, const double* src, int64_t n) {
+  const int64_t min_part = (int64_t)1 << 20;  // 8 MiB per thread at least
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(8, n / min_part));
+  if (nt == 1) {
+    std::memcpy(dst, src, (size_t)n * sizeof(double));
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t part = (n + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t) {
+    const int64_t a = t * part, b = std::min(n, a + part);
+    if (a < b) th.emplace_back([=]() { std::memcpy(dst + a, src + a, (size_t)(b - a) * sizeof(double)); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// Host matrices to HBM through pinned, double-buffered chunks: host threads
+// fill pinned buffer b with chunk i+1 (from the caller's pageable arrays)
+// while the copy engine moves chunk i and, for the corr/net pair, the
+// interleave kernel packs it into the {corr, net} layout. `net` NULL: a plain
+// copy of `corr` into `dst_plain`.
+static int upload_pinned(nr_ctx* ctx, const double* corr, const double* net, int64_t n_elem, double2* dst_pairs,
+                         double* dst_plain, hipStream_t st) {
+  const int parts = net ? 2 : 1;
+  const int64_t chunk = std::min<int64_t>(n_elem, (int64_t)1 << 23);  // 64 MiB per matrix per chunk
+  double* h[2] = {nullptr, nullptr};
+  double* d[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+    e = hipHostMalloc((void**)&h[b], (size_t)(parts * chunk) * sizeof(double), hipHostMallocDefault);
+    if (e == hipSuccess && net) e = hipMalloc((void**)&d[b], (size_t)(parts * chunk) * sizeof(double));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
+  }
+  int64_t i = 0;
+  for (int64_t o = 0; o < n_elem && e == hipSuccess; o += chunk, ++i) {
+    const int b = (int)(i & 1);
+    const int64_t len = std::min(chunk, n_elem - o);
+    if (i >= 2) e = hipEventSynchronize(ev[b]);  // chunk i-2 has left buffer b
+    if (e != hipSuccess) break;
+    parallel_copy(h[b], corr + o, len);
+    if (net) parallel_copy(h[b] + chunk, net + o, len);
+    if (net) {
+      e = hipMemcpyAsync(d[b], h[b], (size_t)(parts * chunk) * sizeof(double), hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = nr::launch_interleave(d[b], d[b] + chunk, dst_pairs + o, len, st);
+    } else {
+      e = hipMemcpyAsync(dst_plain + o, h[b], (size_t)len * sizeof(double), hipMemcpyHostToDevice, st);
+    }
+    if (e == hipSuccess) e = hipEventRecord(ev[b], st);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  for (int b = 0; b < 2; ++b) {
+    if (h[b]) (void)hipHostFree(h[b]);
+    if (d[b]) (void)hipFree(d[b]);
+    if (ev[b]) (void)hipEventDestroy(ev[b]);
+  }
+  if (e != hipSuccess) return hip_fail(ctx, e, "dataset upload");
+  return NR_OK;
+}
+
 int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const double* data,
                    int64_t n_nodes, int64_t n_samples, int where) {
   if (!ctx) return NR_ERR_INVALID;
@@ -725,26 +787,8 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   if (where == NR_DEVICE) {
     NR_HIP(ctx, nr::launch_interleave(corr, net, ctx->d_pairs, n_elem, ctx->stream));
   } else {
-    // Stream the host matrices through two staging buffers in chunks.
-    const int64_t chunk = std::min<int64_t>(n_elem, (int64_t)1 << 25);  // 256 MiB per matrix
-    double *tc = nullptr, *tn = nullptr;
-    NR_HIP(ctx, hipMalloc((void**)&tc, (size_t)chunk * sizeof(double)));
-    hipError_t e = hipMalloc((void**)&tn, (size_t)chunk * sizeof(double));
-    if (e != hipSuccess) {
-      (void)hipFree(tc);
-      return hip_fail(ctx, e, "hipMalloc staging");
-    }
-    for (int64_t o = 0; o < n_elem && e == hipSuccess; o += chunk) {
-      const int64_t len = std::min(chunk, n_elem - o);
-      e = hipMemcpyAsync(tc, corr + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(tn, net + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
-      if (e == hipSuccess) e = nr::launch_interleave(tc, tn, ctx->d_pairs + o, len, ctx->stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    }
-    (void)hipFree(tc);
-    (void)hipFree(tn);
-    if (e != hipSuccess) return hip_fail(ctx, e, "dataset upload");
+    const int rc = upload_pinned(ctx, corr, net, n_elem, ctx->d_pairs, nullptr, ctx->stream);
+    if (rc) return rc;
   }
   NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream));
   NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 5, ctx->stream));
@@ -753,9 +797,12 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   if (data) {
     const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
     NR_HIP(ctx, hipMalloc((void**)&ctx->d_data, bytes));
-    NR_HIP(ctx, hipMemcpyAsync(ctx->d_data, data, bytes,
-                               where == NR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                               ctx->stream));
+    if (where == NR_DEVICE) {
+      NR_HIP(ctx, hipMemcpyAsync(ctx->d_data, data, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+      const int rc = upload_pinned(ctx, data, nullptr, n_samples * n_nodes, nullptr, ctx->d_data, ctx->stream);
+      if (rc) return rc;
+    }
   }
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->symmetric = (asym & 1) ? 0 : 1;

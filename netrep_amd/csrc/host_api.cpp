@@ -114,6 +114,61 @@ bool interrupt_requested() {
   return fn != nullptr && fn(user) != 0;
 }
 
+// Test datasets uploaded ahead of their PermutationProcedure calls
+// (netrep_PrefetchTestDataset): each has its own context on GPU 0, filled by
+// a host thread while the previous dataset's permutations run. At most
+// kMaxPrefetch are pending (the oldest is dropped beyond that).
+struct Prefetch {
+  std::thread th;
+  CtxPtr ctx;
+  const double *data = nullptr, *corr = nullptr, *net = nullptr;
+  int64_t n_samples = 0, n_nodes = 0;
+  std::atomic<int> rc{NR_OK};
+  void join() {
+    if (th.joinable()) th.join();
+  }
+  // at process exit: finish the upload thread, leave the context to the
+  // driver's teardown (the HIP runtime may already be gone)
+  ~Prefetch() {
+    join();
+    (void)ctx.release();
+  }
+};
+constexpr size_t kMaxPrefetch = 2;
+std::mutex g_pf_mu;
+std::vector<std::unique_ptr<Prefetch>> g_pf;
+
+void drop_prefetch(std::unique_ptr<Prefetch>& p) {
+  p->join();
+  p->ctx.reset();  // context destroyed while the runtime is alive
+  p.reset();
+}
+
+// The pending prefetch of exactly these matrices (pointers and sizes), joined
+// and removed from the queue; its context when the upload succeeded.
+CtxPtr take_prefetch(const double* data, const double* corr, const double* net, int64_t n_samples,
+                     int64_t n_nodes) {
+  std::unique_ptr<Prefetch> hit;
+  {
+    std::lock_guard<std::mutex> lk(g_pf_mu);
+    for (size_t i = 0; i < g_pf.size(); ++i) {
+      Prefetch& p = *g_pf[i];
+      if (p.data == data && p.corr == corr && p.net == net && p.n_nodes == n_nodes &&
+          (data == nullptr || p.n_samples == n_samples)) {
+        hit = std::move(g_pf[i]);
+        g_pf.erase(g_pf.begin() + (long)i);
+        break;
+      }
+    }
+  }
+  CtxPtr out;
+  if (!hit) return out;
+  hit->join();
+  if (hit->rc.load() == NR_OK) out = std::move(hit->ctx);
+  drop_prefetch(hit);
+  return out;
+}
+
 // Index sets of the modules present in the test dataset (a4 of SURVEY.md 8).
 struct ModuleSets {
   int32_t n_rows = 0, n_present = 0;
@@ -134,6 +189,45 @@ void netrep_set_interrupt_hook(netrep_interrupt_fn fn, void* user) {
   std::lock_guard<std::mutex> lk(g_hook_mu);
   g_hook = fn;
   g_hook_user = user;
+}
+
+void netrep_DiscardPrefetch(void) {
+  std::vector<std::unique_ptr<Prefetch>> all;
+  {
+    std::lock_guard<std::mutex> lk(g_pf_mu);
+    all.swap(g_pf);
+  }
+  for (auto& p : all) drop_prefetch(p);
+}
+
+int netrep_PrefetchTestDataset(const double* t_data, const double* t_corr, const double* t_net,
+                               int64_t n_samples, int64_t n_nodes) {
+  if (!t_corr || !t_net || n_nodes <= 0 || (t_data && n_samples < 2))
+    return set_err(NR_ERR_INVALID, "invalid arguments to PrefetchTestDataset");
+  std::unique_ptr<Prefetch> p(new Prefetch());
+  const int rc = open_ctx(0, p->ctx);
+  if (rc) return rc;
+  p->data = t_data;
+  p->corr = t_corr;
+  p->net = t_net;
+  p->n_samples = n_samples;
+  p->n_nodes = n_nodes;
+  Prefetch* raw = p.get();
+  raw->th = std::thread([raw]() {
+    raw->rc = nr_set_dataset(raw->ctx.get(), raw->corr, raw->net, raw->data, raw->n_nodes, raw->n_samples,
+                             NR_HOST);
+  });
+  std::unique_ptr<Prefetch> dropped;
+  {
+    std::lock_guard<std::mutex> lk(g_pf_mu);
+    g_pf.push_back(std::move(p));
+    if (g_pf.size() > kMaxPrefetch) {
+      dropped = std::move(g_pf.front());
+      g_pf.erase(g_pf.begin());
+    }
+  }
+  if (dropped) drop_prefetch(dropped);
+  return NR_OK;
 }
 
 int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_data,
@@ -202,7 +296,10 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
   int n_dev = 1;
   const int n_gpu = (n_perm > 0) ? (int)std::min<int64_t>(gpu_count_requested(&n_dev), std::max<int64_t>(n_perm, 1)) : 1;
   std::vector<CtxPtr> ctxs(n_gpu);
-  for (int g = 0; g < n_gpu; ++g) {
+  // a dataset uploaded ahead (netrep_PrefetchTestDataset) becomes GPU 0's
+  ctxs[0] = take_prefetch(t_data, t_corr, t_net, n_samples, n_nodes);
+  const bool prefetched = ctxs[0] != nullptr;
+  for (int g = prefetched ? 1 : 0; g < n_gpu; ++g) {
     int rc = open_ctx(g % n_dev, ctxs[g]);
     if (rc) return rc;
   }
@@ -211,8 +308,8 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
   std::vector<int> rcs(n_gpu, NR_OK);
   auto setup = [&](int g) {
     nr_ctx* c = ctxs[g].get();
-    int rc = g == 0 ? nr_set_dataset(c, t_corr, t_net, t_data, n_nodes, n_samples, NR_HOST)
-                    : nr_copy_dataset(c, ctxs[0].get());
+    int rc = g > 0 ? nr_copy_dataset(c, ctxs[0].get())
+                   : prefetched ? NR_OK : nr_set_dataset(c, t_corr, t_net, t_data, n_nodes, n_samples, NR_HOST);
     if (!rc)
       rc = nr_set_modules(c, ms.n_rows, ms.n_present, ms.row_of.data(), ms.node_off.data(),
                           ms.test_idx.data(), ms.null_pos.data(), ms.disc_cv.data(),

@@ -158,7 +158,7 @@ __device__ __forceinline__ double wd_final(const NetLds& L, int NWn, int c, int 
 // (target ii) parts in LDS, where the targets of one wave instruction are
 // distinct (no same-address atomics). L.idx holds the item's test columns.
 // ---------------------------------------------------------------------------
-template <int NW, int U = 8, int CH = 8>
+template <int NW, int U = 7, int CH = 7>
 __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_local, int64_t off, int64_t k,
                                          const NetLds& L) {
   constexpr int BS = NW * 64;
