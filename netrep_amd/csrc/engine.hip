@@ -158,6 +158,21 @@ __global__ void na_fill_kernel(double* p, int64_t n) {
     p[i] = na;
 }
 
+__global__ void fill_kernel(double* p, int64_t n, double v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+// The Gram's virtual columns behind the resident data block: column N all
+// ones, column N + 1 zeros (ProfileParams::ones_off).
+int fill_virtual_columns(nr_ctx* ctx, int64_t n_nodes, int64_t n_samples) {
+  double* ones = ctx->d_data + n_nodes * n_samples;
+  hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, ctx->stream, ones, n_samples, 1.0);
+  NR_HIP(ctx, hipGetLastError());
+  NR_HIP(ctx, hipMemsetAsync(ones + n_samples, 0, (size_t)n_samples * sizeof(double), ctx->stream));
+  return NR_OK;
+}
+
 int fill_na(nr_ctx* ctx, double* d, int64_t n) {
   if (n <= 0) return NR_OK;
   const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
@@ -469,6 +484,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     nr::ProfileParams pp{};
     pp.data = ctx->d_data;
     pp.n_samples = ctx->n_samples;
+    pp.ones_off = ctx->n_nodes * ctx->n_samples;
     pp.src = src;
     pp.node_off = ctx->d_node_off;
     pp.disc_nc = ctx->d_disc_nc;
@@ -796,7 +812,8 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   NR_HIP(ctx, hipMemcpyAsync(&asym, ctx->d_counters + 5, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   if (data) {
     const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
-    NR_HIP(ctx, hipMalloc((void**)&ctx->d_data, bytes));
+    NR_HIP(ctx, hipMalloc((void**)&ctx->d_data, bytes + 2 * (size_t)n_samples * sizeof(double)));
+    if (int rc = fill_virtual_columns(ctx, n_nodes, n_samples)) return rc;
     if (where == NR_DEVICE) {
       NR_HIP(ctx, hipMemcpyAsync(ctx->d_data, data, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     } else {
@@ -820,13 +837,13 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   dfree(dst->d_data);
   const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2);
   NR_HIP(dst, hipMalloc((void**)&dst->d_pairs, pair_bytes));
-  if (src->d_data) NR_HIP(dst, hipMalloc((void**)&dst->d_data, (size_t)(src->n_samples * src->n_nodes) * sizeof(double)));
+  const size_t data_bytes = (size_t)(src->n_samples * (src->n_nodes + 2)) * sizeof(double);  // + virtual columns
+  if (src->d_data) NR_HIP(dst, hipMalloc((void**)&dst->d_data, data_bytes));
   // Device to device: over xGMI between GPUs, an on-device copy when both
   // contexts share a GPU. The source must be idle (its upload synchronised).
   NR_HIP(dst, hipMemcpyPeerAsync(dst->d_pairs, dst->device, src->d_pairs, src->device, pair_bytes, dst->stream));
   if (src->d_data)
-    NR_HIP(dst, hipMemcpyPeerAsync(dst->d_data, dst->device, src->d_data, src->device,
-                                   (size_t)(src->n_samples * src->n_nodes) * sizeof(double), dst->stream));
+    NR_HIP(dst, hipMemcpyPeerAsync(dst->d_data, dst->device, src->d_data, src->device, data_bytes, dst->stream));
   NR_HIP(dst, hipStreamSynchronize(dst->stream));
   dst->n_nodes = src->n_nodes;
   dst->n_samples = src->n_samples;
@@ -1055,6 +1072,7 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
       nr::ProfileParams pp{};
       pp.data = ctx->d_data;
       pp.n_samples = S;
+      pp.ones_off = ctx->n_nodes * S;
       pp.src = src;
       pp.node_off = d_off;
       pp.n_perm = 1;

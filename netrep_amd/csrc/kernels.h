@@ -50,8 +50,10 @@ struct NetParams {
 };
 
 struct ProfileParams {
-  const double* data;          // n_samples x n_nodes, column-major, scaled
+  const double* data;          // n_samples x (n_nodes + 2), column-major, scaled; column n_nodes
+                               // all ones, n_nodes + 1 zeros (the Gram's virtual columns)
   int64_t n_samples;
+  int64_t ones_off;            // n_nodes * n_samples: offset of the ones column
   IndexSource src;
   const int64_t* node_off;
   const double* disc_nc;       // discovery contribution (NULL: vector mode)

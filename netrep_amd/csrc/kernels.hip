@@ -506,91 +506,82 @@ __device__ __forceinline__ int64_t pk_col(int c, int kc) {
 }
 __device__ __forceinline__ int64_t pk_at(int r, int c, int kc) { return pk_col(c, kc) + (r - c); }
 
-// Loads one 4-row group of an operand column for the Gram MFMA: rows
-// s .. s+3 of a data column, of the virtual all-ones column, or zeros.
-__device__ __forceinline__ void load4(const double* __restrict__ col, bool ones, int s, int S,
-                                      double (&v)[4]) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int r = s + t;
-    v[t] = r < S ? (col ? col[r] : (ones ? 1.0 : 0.0)) : 0.0;
-  }
-}
-
 // G = [X 1]^T [X 1] over the k module columns of X (S x N, column-major) plus a
 // virtual all-ones column at index k, so row k of G holds the column sums;
-// both triangles stored, leading dimension ld >= round32(k + 1). 32 x 32 super-tiles (2 x 2 MFMA tiles of v_mfma_f64_16x16x4_f64) per
-// wave; each lane feeds 4 consecutive rows of every operand column per 16-row
-// step (the K order of the dot products is permuted, identically for both
-// operands). Returns per-lane partial of 1^T G 1 over the X block and a
+// both triangles stored, leading dimension ld >= round32(k + 1), or the packed
+// lower triangle. 32 x 32 super-tiles (2 x 2 MFMA tiles of
+// v_mfma_f64_16x16x4_f64) per wave; each lane feeds 4 consecutive rows of every
+// operand column per 16-row step (the K order of the dot products is permuted,
+// identically for both operands): two 16-byte loads per operand column, the
+// next step's in flight during this step's 16 MFMAs. The ones column and the
+// zero padding columns are real columns of the resident data block (N and
+// N + 1, written at upload), so every lane loads unconditionally; only the
+// last step (S not a multiple of 16) guards its rows. Non-finite data shows
+// on G's diagonal (G_cc = sum of squares of column c), checked in the
+// epilogue. Returns the per-lane part of 1^T G 1 over the X block and a
 // non-finite flag.
 template <int NW = NR_WAVES, bool PACKED = false>
-__device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* idx, int k,
+__device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* idx, int k, int64_t ones_off,
                           double* __restrict__ G, int ld, double& g1sum, int& bad) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, kk = lane >> 4;
   const int kc = k + 1;
   const int T2 = (kc + 31) / 32;
   const int nsup = T2 * (T2 + 1) / 2;
+  const int full = S / 16 * 16;  // steps whose 16 rows are all in range
   for (int t = wave; t < nsup; t += NW) {
     int I2 = 0, rem = t;
     while (rem >= T2 - I2) { rem -= T2 - I2; ++I2; }
     const int J2 = I2 + rem;
-    int cols[4] = {I2 * 32 + i16, I2 * 32 + 16 + i16, J2 * 32 + i16, J2 * 32 + 16 + i16};
-    const double* ptr[4];
-    bool ones[4];
+    const double* col[4];
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
-      ptr[o] = cols[o] < k ? X + (int64_t)idx[cols[o]] * S : nullptr;
-      ones[o] = cols[o] == k;
+      const int c = (o < 2 ? I2 : J2) * 32 + (o & 1) * 16 + i16;
+      const int64_t off = c < k ? (int64_t)idx[c] * S : (c == k ? ones_off : ones_off + S);
+      col[o] = X + off + 4 * kk;
     }
     nr_f64x4 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
-    double cur[4][4];
-    if (PACKED) {
-      // register-lean: no software prefetch (two 8-wave workgroups per CU hide latency)
-      for (int s0 = 0; s0 < S; s0 += 16) {
+    auto ld16 = [&](int s0, double (&v)[4][4]) {
 #pragma unroll
-        for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], s0 + 4 * kk, S, cur[o]);
-#pragma unroll
-        for (int o = 0; o < 4; ++o)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[2][q], acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[3][q], acc[1][1], 0, 0, 0);
-        }
+      for (int o = 0; o < 4; ++o) {
+        double2 p0, p1;
+        __builtin_memcpy(&p0, col[o] + s0, sizeof(double2));
+        __builtin_memcpy(&p1, col[o] + s0 + 2, sizeof(double2));
+        v[o][0] = p0.x;
+        v[o][1] = p0.y;
+        v[o][2] = p1.x;
+        v[o][3] = p1.y;
       }
-    } else {
-      double nxt[4][4];
+    };
+    auto mfma16 = [&](const double (&v)[4][4]) {
 #pragma unroll
-      for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], 4 * kk, S, cur[o]);
-      for (int s0 = 0; s0 < S; s0 += 16) {
-        const int sn = s0 + 16 + 4 * kk;
-#pragma unroll
-        for (int o = 0; o < 4; ++o) load4(ptr[o], ones[o], sn, S, nxt[o]);
-#pragma unroll
-        for (int o = 0; o < 4; ++o)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[2][q], acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[1][q], cur[3][q], acc[1][1], 0, 0, 0);
-        }
-#pragma unroll
-        for (int o = 0; o < 4; ++o)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+      for (int q = 0; q < 4; ++q) {
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[0][q], v[2][q], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[0][q], v[3][q], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[1][q], v[2][q], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[1][q], v[3][q], acc[1][1], 0, 0, 0);
       }
+    };
+    double cur[4][4], nxt[4][4];
+    if (full > 0) ld16(0, cur);
+    for (int s0 = 0; s0 < full; s0 += 16) {
+      if (s0 + 16 < full) ld16(s0 + 16, nxt);
+      mfma16(cur);
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+    }
+    if (full < S) {  // the last, partial step
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[o][q] = full + 4 * kk + q < S ? col[o][full + q] : 0.0;
+      mfma16(cur);
     }
     if (PACKED && t == 0 && lane == 0) G[pk_col(kc, kc)] = 0.0;  // zero pad read by packed_matvec
     const double wgt = (I2 == J2) ? 1.0 : 2.0;
@@ -611,6 +602,7 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
             G[gj + (int64_t)gi * ld] = val;
           }
           if (gi < k && gj < k) g1sum += wgt * val;
+          if (gi == gj && gi < k) bad |= (int)!isfinite(val);
         }
   }
 }
@@ -625,7 +617,8 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
 // samples and nodes exchanged: operand columns are samples (16 consecutive
 // samples of one node per lane group: one 128-byte read), the contraction
 // runs over the nodes. Returns the per-lane part of |X 1|^2 (= 1'G1 of the
-// primal Gram; here the squared norm of H's ones column) and a non-finite flag.
+// primal Gram; here the squared norm of H's ones column) and a non-finite flag
+// (from H's diagonal).
 template <int NW = NR_WAVES, bool PACKED = false>
 __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32_t* idx, int k,
                                double* __restrict__ G, int ld, double& g1sum, int& bad) {
@@ -659,10 +652,6 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
     for (int c0 = 0; c0 < k; c0 += 16) {
       if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
 #pragma unroll
-      for (int o = 0; o < 4; ++o)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bad |= !isfinite(cur[o][q]);
-#pragma unroll
       for (int q = 0; q < 4; ++q) {
         acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[2][q], acc[0][0], 0, 0, 0);
         acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[0][q], cur[3][q], acc[0][1], 0, 0, 0);
@@ -691,6 +680,7 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
             G[gj + (int64_t)gi * ld] = val;
           }
           if (gj == S && gi < S) g1sum += val * val;  // |X 1|^2 from the row sums (X 1)_gi
+          if (gi == gj && gi < S) bad |= (int)!isfinite(val);  // H_ss: squares of sample s's values
         }
   }
 }
@@ -1060,7 +1050,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     if (dual)
       gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, ld, g1[0], bad);
     else
-      gram_mfma<NW, PACKED>(X, S, L.idx, k, G, ld, g1[0], bad);
+      gram_mfma<NW, PACKED>(X, S, L.idx, k, P.ones_off, G, ld, g1[0], bad);
     if (bad) atomicOr(&s_flags[1], 1);
     block_sums<1, NW>(g1, L.red);  // barriers also publish G to the whole workgroup
     NR_STAMP(1);  // Gram
