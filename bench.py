@@ -346,7 +346,8 @@ def main():
         roofline = {"kernel": dom_name, "bound": dom["bound"], "achieved": round(dom["achieved"], 4),
                     "peak": dom["peak"], "unit": dom["unit"], "frac": round(dom["frac"], 6),
                     "traffic": measured_traffic(args.config, B, dom_name),
-                    "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, profiles/pmc_traffic.json)",
+                    "traffic_unit": "L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 "
+                                    "+ WRITE_SIZE, profiles/pmc_traffic.json)",
                     "algorithmic_bytes": round(((net_b if fused or dom_name == "module_net_kernel" else 0.0)
                                                 + (prof_b if dom_name == "module_profile_kernel" else 0.0)) * B)}
         cpu = None
