@@ -66,6 +66,22 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net,
 /* Make src's resident dataset resident in dst too, device to device (over
  * xGMI when the contexts are on different GPUs): the host matrices cross PCIe
  * once, to the first GPU, and fan out from there. */
+/* disk.matrix files straight to HBM (R/disk-matrix-class.R:175-182 reads them
+ * back with readRDS): numeric matrices serialised by saveRDS (gzip or
+ * uncompressed, XDR format 2/3) or objects of a save() archive (`*_object`,
+ * NULL: the first numeric matrix). The payload is read straight into pinned
+ * buffers and converted from big-endian on the device; `data` (samples x
+ * nodes, NULL for the network-only path) is scaled there as Scale does
+ * (src/scale.cpp:14-25) when scale_data != 0. The network file's column names
+ * become the dataset's node names (nr_dataset_colnames). */
+int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_path, const char* data_path,
+                         const char* corr_object, const char* net_object, const char* data_object,
+                         int scale_data);
+int nr_dataset_shape(const nr_ctx* ctx, int64_t* n_nodes, int64_t* n_samples);
+/* NUL-separated node names of a dataset loaded from files; *needed = bytes
+ * (written only when cap >= *needed). */
+int nr_dataset_colnames(const nr_ctx* ctx, char* buf, int64_t cap, int64_t* needed);
+
 int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src);
 
 /* 1 if corr and net of the resident dataset are exactly symmetric. */
@@ -246,6 +262,26 @@ int netrep_PermutationProcedure(
 int netrep_PrefetchTestDataset(const double* t_data, const double* t_corr, const double* t_net,
                                int64_t n_samples, int64_t n_nodes);
 void netrep_DiscardPrefetch(void);
+
+/* PermutationProcedure with the test dataset given as disk.matrix files
+ * (R/disk-matrix-class.R; the R code would otherwise loadIntoRAM() them,
+ * R/modulePreservation.R:553-620): the files go straight to GPU 0's HBM,
+ * tData is scaled there, and the node names are the network file's column
+ * names. Other arguments and outputs as netrep_PermutationProcedure. */
+int netrep_PermutationProcedureFiles(const netrep_disc_props* disc_props, const char* t_data_file,
+                                     const char* t_corr_file, const char* t_net_file,
+                                     const char* const* ma_names, const char* const* ma_labels,
+                                     int64_t n_assign, const char* const* modules, int64_t n_modules,
+                                     int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
+                                     int32_t verbose, uint64_t seed, const uint32_t* pi,
+                                     double* nulls_out, double* observed_out);
+
+/* Host read of one numeric matrix from an RDS file or save() archive (the
+ * same reader): dims always; values (column-major, native) into `out` when
+ * non-NULL; NUL-separated column names into `colnames` when cap suffices
+ * (*colnames_needed = bytes). No GPU involved. */
+int netrep_ReadRDSMatrix(const char* path, const char* object, int64_t* nrow, int64_t* ncol, double* out,
+                         char* colnames, int64_t colnames_cap, int64_t* colnames_needed);
 
 /* IntermediateProperties[NoData] (src/discProps.cpp:44-48, :171-175).
  * Outputs per module in `modules` order, concatenated; lengths written to

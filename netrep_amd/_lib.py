@@ -94,6 +94,14 @@ SIGNATURES = {
     "netrep_last_error": (C.c_char_p, []),
     "netrep_set_interrupt_hook": (None, [C.c_void_p, C.c_void_p]),
     "netrep_PrefetchTestDataset": (_int, [_dp, _dp, _dp, _i64, _i64]),
+    "nr_set_dataset_files": (_int, [_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                    C.c_char_p, _int]),
+    "nr_dataset_shape": (_int, [_p, _i64p, _i64p]),
+    "nr_dataset_colnames": (_int, [_p, C.c_char_p, _i64, _i64p]),
+    "netrep_PermutationProcedureFiles": (_int, [C.POINTER(DiscProps), C.c_char_p, C.c_char_p, C.c_char_p,
+                                                _strv, _strv, _i64, _strv, _i64, _i64, _i32, C.c_char_p,
+                                                _i32, _u64, _u32p, _dp, _dp]),
+    "netrep_ReadRDSMatrix": (_int, [C.c_char_p, C.c_char_p, _i64p, _i64p, _dp, C.c_char_p, _i64, _i64p]),
     "netrep_DiscardPrefetch": (None, []),
 }
 

@@ -292,6 +292,82 @@ def PermutationProcedure(discProps: dict, tData: RMatrix, tCorr: RMatrix, tNet: 
                         nCores, nullHypothesis, verbose, seed, pi)
 
 
+def read_rds_matrix(path: str, object: Optional[str] = None) -> RMatrix:
+    """One numeric matrix from an RDS file (saveRDS, gzip or uncompressed) or,
+    by name, a save() archive -- what disk.matrix holds
+    (R/disk-matrix-class.R:175-182) -- via netrep_ReadRDSMatrix (host read)."""
+    lib = L.load()
+    nrow, ncol, need = C.c_int64(), C.c_int64(), C.c_int64()
+    p = str(path).encode()
+    o = None if object is None else str(object).encode()
+    L.check_api(lib.netrep_ReadRDSMatrix(p, o, C.byref(nrow), C.byref(ncol), None, None, 0, C.byref(need)))
+    out = np.empty((nrow.value, ncol.value), order="F")
+    buf = C.create_string_buffer(max(need.value, 1))
+    L.check_api(lib.netrep_ReadRDSMatrix(p, o, C.byref(nrow), C.byref(ncol), _dptr(out), buf, need.value,
+                                         C.byref(need)))
+    names = [x.decode() for x in buf.raw[:need.value].split(b"\0")[:-1]] if need.value else None
+    return RMatrix(out, None, names)
+
+
+def PermutationProcedureFiles(discProps: dict, tData_file: Optional[str], tCorr_file: str, tNet_file: str,
+                              moduleAssignments, modules, nPermutations: int, nCores: int = 1,
+                              nullHypothesis: str = "overlap", verbose: bool = False,
+                              seed: int = DEFAULT_SEED, pi=None) -> dict:
+    """PermutationProcedure[NoData] on a test dataset held as disk.matrix files
+    (netrep_PermutationProcedureFiles): the files go straight to HBM and tData
+    (raw, unscaled) is scaled on the device; node names are the network file's
+    column names."""
+    lib = L.load()
+    names, labels = _assignments(moduleAssignments)
+    modules = [str(m) for m in modules]
+    with_data = tData_file is not None
+    nm_ = len(modules)
+    keep = []
+
+    def vecs(key):
+        d = discProps.get(key, {}) if discProps is not None else {}
+        ptrs = (C.POINTER(C.c_double) * max(nm_, 1))()
+        lens = np.zeros(max(nm_, 1), dtype=np.int64)
+        for i, m in enumerate(modules):
+            if m in d:
+                v = np.ascontiguousarray(d[m], dtype=np.float64)
+                keep.append(v)
+                ptrs[i] = _dptr(v)
+                lens[i] = v.size
+        keep.append(lens)
+        return ptrs, lens.ctypes.data_as(C.POINTER(C.c_int64))
+
+    dp = L.DiscProps()
+    dp.degree, dp.degree_len = vecs("degree")
+    dp.corr, dp.corr_len = vecs("corr")
+    if with_data:
+        dp.contribution, dp.contribution_len = vecs("contribution")
+    n_stat = 7 if with_data else 4
+    observed = np.empty((nm_, n_stat), order="F")
+    nulls = np.empty((nm_, n_stat, int(nPermutations)), order="F") if nPermutations > 0 else None
+    pi_arr = None if pi is None else np.ascontiguousarray(pi, dtype=np.uint32)
+    an, _k2 = _strv(names)
+    al, _k3 = _strv(labels)
+    mo, _k4 = _strv(modules)
+    enc = lambda x: None if x is None else str(x).encode()  # noqa: E731
+    rc = lib.netrep_PermutationProcedureFiles(
+        C.byref(dp), enc(tData_file), enc(tCorr_file), enc(tNet_file), an, al, len(names), mo, nm_,
+        int(nPermutations), int(nCores), str(nullHypothesis).encode(), int(bool(verbose)),
+        int(seed) & (2**64 - 1), pi_arr.ctypes.data_as(C.POINTER(C.c_uint32)) if pi_arr is not None else None,
+        _dptr(nulls), _dptr(observed))
+    interrupted = rc == L.NR_ERR_CANCELLED
+    if not interrupted:
+        L.check_api(rc)
+    statnames = STATNAMES if with_data else STATNAMES_NODATA
+    res = {"observed": observed, "observed_dimnames": (modules, statnames)}
+    if interrupted:
+        res["interrupted"] = True
+    if nPermutations > 0:
+        res["nulls"] = nulls
+        res["nulls_dimnames"] = (modules, statnames, None)
+    return res
+
+
 def PermutationProcedureNoData(discProps: dict, tCorr: RMatrix, tNet: RMatrix, moduleAssignments,
                                modules, nPermutations: int, nCores: int = 1,
                                nullHypothesis: str = "overlap", verbose: bool = False,

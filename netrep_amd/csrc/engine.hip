@@ -22,6 +22,7 @@
 #include "../../include/netrep_gpu.h"
 #include "kernels.h"
 #include "prp.h"
+#include "rds_reader.h"
 
 namespace {
 
@@ -52,6 +53,7 @@ struct nr_ctx {
   double2* d_pairs = nullptr;
   double* d_data = nullptr;
   int64_t n_nodes = 0, n_samples = 0;
+  std::vector<std::string> node_names;  // column names of a dataset loaded from files
   int symmetric = 0;
   int corr_finite = 0, net_finite = 0;  // CheckFinite of the resident matrices
 
@@ -796,6 +798,7 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   dfree(ctx->d_pairs);
   dfree(ctx->d_data);
+  ctx->node_names.clear();
   ctx->n_nodes = n_nodes;
   ctx->n_samples = data ? n_samples : 0;
   const int64_t n_elem = n_nodes * n_nodes;
@@ -828,6 +831,137 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   return NR_OK;
 }
 
+// File -> pinned -> HBM for one matrix payload: the host inflates / reads
+// straight into pinned buffer b while the copy engine moves the previous one
+// and a kernel converts it from XDR into `pairs` (half 0 / 1) or `plain`.
+static int upload_file_matrix(nr_ctx* ctx, nr::RMatrixReader& rd, double2* pairs, int half, double* plain,
+                              hipStream_t st) {
+  const int64_t n = rd.length();
+  const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), (int64_t)1 << 23);  // 64 MiB
+  double* h[2] = {nullptr, nullptr};
+  double* d[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+    e = hipHostMalloc((void**)&h[b], (size_t)chunk * sizeof(double), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void**)&d[b], (size_t)chunk * sizeof(double));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
+  }
+  bool read_ok = true;
+  int64_t i = 0;
+  for (int64_t o = 0; o < n && e == hipSuccess && read_ok; o += chunk, ++i) {
+    const int b = (int)(i & 1);
+    const int64_t len = std::min(chunk, n - o);
+    if (i >= 2) e = hipEventSynchronize(ev[b]);
+    if (e != hipSuccess) break;
+    read_ok = rd.read_raw(h[b], len);
+    if (!read_ok) break;
+    e = hipMemcpyAsync(d[b], h[b], (size_t)len * sizeof(double), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = nr::launch_xdr(d[b], pairs ? pairs + o : nullptr, half, plain ? plain + o : nullptr, len, st);
+    if (e == hipSuccess) e = hipEventRecord(ev[b], st);
+  }
+  const hipError_t e2 = hipStreamSynchronize(st);
+  if (e == hipSuccess) e = e2;
+  for (int b = 0; b < 2; ++b) {
+    if (h[b]) (void)hipHostFree(h[b]);
+    if (d[b]) (void)hipFree(d[b]);
+    if (ev[b]) (void)hipEventDestroy(ev[b]);
+  }
+  if (!read_ok) return fail(ctx, NR_ERR_INVALID, rd.error());
+  if (e != hipSuccess) return hip_fail(ctx, e, "file upload");
+  return NR_OK;
+}
+
+int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_path, const char* data_path,
+                         const char* corr_object, const char* net_object, const char* data_object,
+                         int scale_data) {
+  if (!ctx) return NR_ERR_INVALID;
+  if (!corr_path || !net_path) return fail(ctx, NR_ERR_INVALID, "corr/net file missing");
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  nr::RMatrixReader rc_, rn_;
+  if (!rc_.open(corr_path, corr_object)) return fail(ctx, NR_ERR_INVALID, std::string(corr_path) + ": " + rc_.error());
+  if (!rn_.open(net_path, net_object)) return fail(ctx, NR_ERR_INVALID, std::string(net_path) + ": " + rn_.error());
+  const int64_t n_elem = rc_.length();
+  int64_t n_nodes = (int64_t)std::llround(std::sqrt((double)n_elem));
+  if (n_nodes <= 0 || n_nodes * n_nodes != n_elem) return fail(ctx, NR_ERR_INVALID, "correlation matrix is not square");
+  if (rn_.length() != n_elem) return fail(ctx, NR_ERR_INVALID, "network and correlation matrices differ in size");
+  if (n_nodes > (int64_t)INT32_MAX) return fail(ctx, NR_ERR_UNSUPPORTED, "n_nodes exceeds 2^31-1");
+  dfree(ctx->d_pairs);
+  dfree(ctx->d_data);
+  ctx->node_names.clear();
+  NR_HIP(ctx, hipMalloc((void**)&ctx->d_pairs, (size_t)n_elem * sizeof(double2)));
+  int rc;
+  nr::RMatrixMeta mc, mn;
+  if ((rc = upload_file_matrix(ctx, rc_, ctx->d_pairs, 0, nullptr, ctx->stream))) return rc;
+  if (!rc_.finish(&mc)) return fail(ctx, NR_ERR_INVALID, std::string(corr_path) + ": " + rc_.error());
+  if ((rc = upload_file_matrix(ctx, rn_, ctx->d_pairs, 1, nullptr, ctx->stream))) return rc;
+  if (!rn_.finish(&mn)) return fail(ctx, NR_ERR_INVALID, std::string(net_path) + ": " + rn_.error());
+  if (mc.nrow != n_nodes || mc.ncol != n_nodes || mn.nrow != n_nodes || mn.ncol != n_nodes)
+    return fail(ctx, NR_ERR_INVALID, "correlation / network matrices must be square and of one size");
+  ctx->node_names = !mn.colnames.empty() ? mn.colnames : mc.colnames;
+  int64_t n_samples = 0;
+  if (data_path) {
+    nr::RMatrixReader rd;
+    if (!rd.open(data_path, data_object)) return fail(ctx, NR_ERR_INVALID, std::string(data_path) + ": " + rd.error());
+    if (rd.length() % n_nodes != 0) return fail(ctx, NR_ERR_INVALID, "data matrix columns do not match the network");
+    n_samples = rd.length() / n_nodes;
+    if (n_samples < 2) return fail(ctx, NR_ERR_INVALID, "data needs n_samples >= 2");
+    double* raw = nullptr;
+    NR_HIP(ctx, hipMalloc((void**)&raw, (size_t)rd.length() * sizeof(double)));
+    rc = upload_file_matrix(ctx, rd, nullptr, 0, raw, ctx->stream);
+    nr::RMatrixMeta md;
+    if (!rc && !rd.finish(&md)) rc = fail(ctx, NR_ERR_INVALID, std::string(data_path) + ": " + rd.error());
+    if (!rc && (md.nrow != n_samples || md.ncol != n_nodes))
+      rc = fail(ctx, NR_ERR_INVALID, "data matrix must be samples x nodes");
+    hipError_t e = hipSuccess;
+    if (!rc) e = hipMalloc((void**)&ctx->d_data, (size_t)(n_samples * (n_nodes + 2)) * sizeof(double));
+    // Scale (src/scale.cpp:14-25) on the device, as the R code scales after loading
+    if (!rc && e == hipSuccess)
+      e = scale_data ? nr::launch_scale(raw, ctx->d_data, n_samples, n_nodes, ctx->stream)
+                     : hipMemcpyAsync(ctx->d_data, raw, (size_t)(n_samples * n_nodes) * sizeof(double),
+                                      hipMemcpyDeviceToDevice, ctx->stream);
+    if (!rc && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(raw);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(ctx, e, "data upload");
+    ctx->n_samples = n_samples;
+    ctx->n_nodes = n_nodes;
+    if ((rc = fill_virtual_columns(ctx, n_nodes, n_samples))) return rc;
+  }
+  ctx->n_nodes = n_nodes;
+  ctx->n_samples = n_samples;
+  NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream));
+  NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 5, ctx->stream));
+  int asym = 0;
+  NR_HIP(ctx, hipMemcpyAsync(&asym, ctx->d_counters + 5, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->symmetric = (asym & 1) ? 0 : 1;
+  ctx->corr_finite = (asym & 2) ? 0 : 1;
+  ctx->net_finite = (asym & 4) ? 0 : 1;
+  return NR_OK;
+}
+
+int nr_dataset_shape(const nr_ctx* ctx, int64_t* n_nodes, int64_t* n_samples) {
+  if (!ctx) return NR_ERR_INVALID;
+  if (n_nodes) *n_nodes = ctx->n_nodes;
+  if (n_samples) *n_samples = ctx->n_samples;
+  return NR_OK;
+}
+
+int nr_dataset_colnames(const nr_ctx* ctx, char* buf, int64_t cap, int64_t* needed) {
+  if (!ctx || !needed) return NR_ERR_INVALID;
+  int64_t total = 0;
+  for (const std::string& s : ctx->node_names) total += (int64_t)s.size() + 1;
+  *needed = total;
+  if (!buf || cap < total) return NR_OK;
+  for (const std::string& s : ctx->node_names) {
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    buf += s.size() + 1;
+  }
+  return NR_OK;
+}
+
 int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   if (!dst || !src || dst == src) return NR_ERR_INVALID;
   if (!src->d_pairs) return fail(dst, NR_ERR_INVALID, "source context has no dataset");
@@ -847,6 +981,7 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   NR_HIP(dst, hipStreamSynchronize(dst->stream));
   dst->n_nodes = src->n_nodes;
   dst->n_samples = src->n_samples;
+  dst->node_names = src->node_names;
   dst->symmetric = src->symmetric;
   dst->corr_finite = src->corr_finite;
   dst->net_finite = src->net_finite;

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/netrep_gpu.h"
+#include "rds_reader.h"
 
 namespace {
 
@@ -230,19 +231,18 @@ int netrep_PrefetchTestDataset(const double* t_data, const double* t_corr, const
   return NR_OK;
 }
 
-int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_data,
-                                const double* t_corr, const double* t_net, int64_t n_samples,
-                                int64_t n_nodes, const char* const* t_names,
-                                const char* const* ma_names, const char* const* ma_labels,
-                                int64_t n_assign, const char* const* modules, int64_t n_modules,
-                                int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
-                                int32_t verbose, uint64_t seed, const uint32_t* pi,
-                                double* nulls_out, double* observed_out) {
-  (void)n_cores;
-  if (!disc || !t_corr || !t_net || !t_names || !ma_names || !ma_labels || !modules ||
-      !observed_out || n_perm < 0 || (n_perm > 0 && !nulls_out) || n_nodes <= 0)
-    return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedure");
-  const bool with_data = t_data != nullptr;
+}  // extern "C"
+
+namespace {
+
+// PermutationProcedure with the dataset given either as host matrices or as a
+// context that already holds it (`preloaded`: a prefetch or a file load).
+int permutation_impl(const netrep_disc_props* disc, bool with_data, const double* t_data,
+                     const double* t_corr, const double* t_net, int64_t n_samples, int64_t n_nodes,
+                     const char* const* t_names, const char* const* ma_names, const char* const* ma_labels,
+                     int64_t n_assign, const char* const* modules, int64_t n_modules, int64_t n_perm,
+                     const char* null_hypothesis, int32_t verbose, uint64_t seed, const uint32_t* pi,
+                     double* nulls_out, double* observed_out, CtxPtr preloaded) {
   if (with_data && !disc->contribution)
     return set_err(NR_ERR_INVALID, "discProps has no 'contribution' but tData was given");
   const std::string null_type = null_hypothesis ? null_hypothesis : "overlap";
@@ -296,8 +296,8 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
   int n_dev = 1;
   const int n_gpu = (n_perm > 0) ? (int)std::min<int64_t>(gpu_count_requested(&n_dev), std::max<int64_t>(n_perm, 1)) : 1;
   std::vector<CtxPtr> ctxs(n_gpu);
-  // a dataset uploaded ahead (netrep_PrefetchTestDataset) becomes GPU 0's
-  ctxs[0] = take_prefetch(t_data, t_corr, t_net, n_samples, n_nodes);
+  // a dataset already resident (prefetched or loaded from files) becomes GPU 0's
+  ctxs[0] = std::move(preloaded);
   const bool prefetched = ctxs[0] != nullptr;
   for (int g = prefetched ? 1 : 0; g < n_gpu; ++g) {
     int rc = open_ctx(g % n_dev, ctxs[g]);
@@ -397,6 +397,82 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
     if (rcs[g]) return ctx_err(rcs[g], ctxs[g].get());
   }
   if (cancelled_at >= 0) return ctx_err(NR_ERR_CANCELLED, ctxs[cancelled_at].get());
+  return NR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_data,
+                                const double* t_corr, const double* t_net, int64_t n_samples,
+                                int64_t n_nodes, const char* const* t_names,
+                                const char* const* ma_names, const char* const* ma_labels,
+                                int64_t n_assign, const char* const* modules, int64_t n_modules,
+                                int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
+                                int32_t verbose, uint64_t seed, const uint32_t* pi,
+                                double* nulls_out, double* observed_out) {
+  (void)n_cores;
+  if (!disc || !t_corr || !t_net || !t_names || !ma_names || !ma_labels || !modules ||
+      !observed_out || n_perm < 0 || (n_perm > 0 && !nulls_out) || n_nodes <= 0)
+    return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedure");
+  // a dataset uploaded ahead (netrep_PrefetchTestDataset) is adopted
+  CtxPtr pre = take_prefetch(t_data, t_corr, t_net, n_samples, n_nodes);
+  return permutation_impl(disc, t_data != nullptr, t_data, t_corr, t_net, n_samples, n_nodes, t_names, ma_names,
+                          ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose, seed, pi,
+                          nulls_out, observed_out, std::move(pre));
+}
+
+int netrep_PermutationProcedureFiles(const netrep_disc_props* disc, const char* t_data_file,
+                                     const char* t_corr_file, const char* t_net_file,
+                                     const char* const* ma_names, const char* const* ma_labels,
+                                     int64_t n_assign, const char* const* modules, int64_t n_modules,
+                                     int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
+                                     int32_t verbose, uint64_t seed, const uint32_t* pi,
+                                     double* nulls_out, double* observed_out) {
+  (void)n_cores;
+  if (!disc || !t_corr_file || !t_net_file || !ma_names || !ma_labels || !modules || !observed_out ||
+      n_perm < 0 || (n_perm > 0 && !nulls_out))
+    return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedureFiles");
+  CtxPtr ctx;
+  int rc = open_ctx(0, ctx);
+  if (rc) return rc;
+  // disk.matrix files straight to HBM; tData scaled on the device
+  rc = nr_set_dataset_files(ctx.get(), t_corr_file, t_net_file, t_data_file, nullptr, nullptr, nullptr, 1);
+  if (rc) return ctx_err(rc, ctx.get());
+  int64_t n_nodes = 0, n_samples = 0, need = 0;
+  nr_dataset_shape(ctx.get(), &n_nodes, &n_samples);
+  nr_dataset_colnames(ctx.get(), nullptr, 0, &need);
+  std::vector<char> buf((size_t)std::max<int64_t>(need, 1));
+  nr_dataset_colnames(ctx.get(), buf.data(), need, &need);
+  std::vector<const char*> names;
+  for (int64_t o = 0; o < need; o += (int64_t)std::strlen(buf.data() + o) + 1) names.push_back(buf.data() + o);
+  if ((int64_t)names.size() != n_nodes)
+    return set_err(NR_ERR_INVALID, "the network file has no column names (node names are needed)");
+  return permutation_impl(disc, t_data_file != nullptr, nullptr, nullptr, nullptr, n_samples, n_nodes, names.data(),
+                          ma_names, ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose,
+                          seed, pi, nulls_out, observed_out, std::move(ctx));
+}
+
+int netrep_ReadRDSMatrix(const char* path, const char* object, int64_t* nrow, int64_t* ncol, double* out,
+                         char* colnames, int64_t colnames_cap, int64_t* colnames_needed) {
+  if (!path || !nrow || !ncol) return set_err(NR_ERR_INVALID, "invalid arguments to ReadRDSMatrix");
+  nr::RMatrixMeta meta;
+  std::vector<double> v;
+  std::string err;
+  if (!nr::read_matrix_host(path, object, &meta, &v, out != nullptr, &err))
+    return set_err(NR_ERR_INVALID, std::string(path) + ": " + err);
+  *nrow = meta.nrow;
+  *ncol = meta.ncol;
+  if (out) std::memcpy(out, v.data(), v.size() * sizeof(double));
+  int64_t total = 0;
+  for (const std::string& s : meta.colnames) total += (int64_t)s.size() + 1;
+  if (colnames_needed) *colnames_needed = total;
+  if (colnames && colnames_cap >= total)
+    for (const std::string& s : meta.colnames) {
+      std::memcpy(colnames, s.c_str(), s.size() + 1);
+      colnames += s.size() + 1;
+    }
   return NR_OK;
 }
 

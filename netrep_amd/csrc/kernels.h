@@ -102,6 +102,8 @@ hipError_t launch_interleave(const double* corr, const double* net, double2* out
                              hipStream_t st);
 hipError_t launch_symmetry(const double2* a, int64_t n, int* asym, hipStream_t st);
 hipError_t launch_scale(const double* in, double* out, int64_t S, int64_t N, hipStream_t st);
+// XDR (big-endian) doubles -> native: into pairs[i].x (half 0) / .y (half 1), or `plain`
+hipError_t launch_xdr(const void* raw, double2* pairs, int half, double* plain, int64_t n, hipStream_t st);
 hipError_t launch_finite(const double* a, int64_t n, int* nonfinite, hipStream_t st);
 hipError_t launch_export(const IndexSource& src, int64_t n_nodes_total, int32_t* out,
                          int64_t n_perm, hipStream_t st);

@@ -12,6 +12,7 @@
 // IntermediateProperties (src/discProps.cpp:100-121) and NetProps
 // (src/properties.cpp:155-184).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include <math.h>
 
@@ -1481,6 +1482,20 @@ module_profile_reg_kernel(ProfileParams P) {
 // ---------------------------------------------------------------------------
 
 // {corr, net} interleave (one 16-byte element per (i, j)).
+// Big-endian (XDR) doubles of an R serialisation stream into native ones:
+// into one half of the {corr, net} pairs (half 0 / 1) or a plain array.
+__global__ void xdr_pairs_kernel(const unsigned long long* __restrict__ raw, double2* __restrict__ pairs,
+                                 int64_t n, int half) {
+  double* dst = reinterpret_cast<double*>(pairs) + half;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[2 * i] = __longlong_as_double((long long)__builtin_bswap64(raw[i]));
+}
+
+__global__ void xdr_plain_kernel(const unsigned long long* __restrict__ raw, double* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = __longlong_as_double((long long)__builtin_bswap64(raw[i]));
+}
+
 __global__ void interleave_kernel(const double* __restrict__ corr, const double* __restrict__ net,
                                   double2* __restrict__ out, int64_t n_elem) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_elem;
@@ -1674,6 +1689,15 @@ hipError_t launch_interleave(const double* corr, const double* net, double2* out
 hipError_t launch_symmetry(const double2* a, int64_t n, int* asym, hipStream_t st) {
   const unsigned nb = (unsigned)((n + 31) / 32);
   hipLaunchKernelGGL(symmetry_kernel, dim3(nb, nb), dim3(256), 0, st, a, n, asym);
+  return hipGetLastError();
+}
+
+hipError_t launch_xdr(const void* raw, double2* pairs, int half, double* plain, int64_t n, hipStream_t st) {
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+  if (pairs)
+    hipLaunchKernelGGL(xdr_pairs_kernel, dim3(g), dim3(256), 0, st, (const unsigned long long*)raw, pairs, n, half);
+  else
+    hipLaunchKernelGGL(xdr_plain_kernel, dim3(g), dim3(256), 0, st, (const unsigned long long*)raw, plain, n);
   return hipGetLastError();
 }
 

@@ -81,6 +81,27 @@ class Engine:
         self.n_nodes = n
         self.n_samples = s
 
+    def set_dataset_files(self, corr_path, net_path, data_path=None, objects=(None, None, None),
+                          scale_data=True):
+        """disk.matrix files (saveRDS output, or objects of a save() archive)
+        straight to HBM; `data` is scaled on the device. Returns the node names
+        (the network file's column names)."""
+        enc = lambda x: None if x is None else str(x).encode()  # noqa: E731
+        self._check(self._lib.nr_set_dataset_files(self._h, enc(corr_path), enc(net_path), enc(data_path),
+                                                   enc(objects[0]), enc(objects[1]), enc(objects[2]),
+                                                   int(bool(scale_data))))
+        n, s_ = C.c_int64(), C.c_int64()
+        self._check(self._lib.nr_dataset_shape(self._h, C.byref(n), C.byref(s_)))
+        need = C.c_int64()
+        self._check(self._lib.nr_dataset_colnames(self._h, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(max(need.value, 1))
+        self._check(self._lib.nr_dataset_colnames(self._h, buf, need.value, C.byref(need)))
+        names = buf.raw[:need.value].split(b"\0")[:-1] if need.value else []
+        self.n_stat = 7 if data_path is not None else 4
+        self.n_nodes = n.value
+        self.n_samples = s_.value
+        return [x.decode() for x in names]
+
     def set_dataset_device(self, corr_ptr: int, net_ptr: int, data_ptr, n_nodes: int, n_samples: int):
         """Device pointers (e.g. torch tensors after an RCCL broadcast). The
         engine reads them on its own stream: the producer's work must be
