@@ -203,6 +203,21 @@ def roofline_terms(sizes, n_samples, with_data):
     return net_bytes, prof_bytes, prof_flops
 
 
+# Random 16-byte gathers over a 6.4 GB matrix on MI355X (tools/probes/gather_probe.hip,
+# profiles/r02/gather_probe.txt): the line rate the network kernel is bound by.
+GATHER_CEILING_GREADS = 50.0
+
+
+def gather_ceiling(sizes, perms, seconds):
+    """The network kernel against the measured random-gather ceiling: one
+    16-byte {corr, net} read per unordered pair of every module."""
+    k = np.asarray(sizes, dtype=np.int64)
+    reads = float((k * (k - 1) // 2).sum()) * perms
+    g = reads / seconds / 1e9
+    return {"achieved": g, "peak": GATHER_CEILING_GREADS, "unit": "G 16-byte reads/s", "frac": g / GATHER_CEILING_GREADS,
+            "source": "profiles/r02/gather_probe.txt"}
+
+
 def time_steps(eng, world, rank, steps, warmup, perms_per_step, seed, base_warm):
     """W untimed warm-up steps, then K steps bracketed by barrier + device
     synchronisation; returns (max-over-ranks seconds, local null chunks, base)."""
@@ -319,6 +334,7 @@ def main():
                              "frac": net_b * B2 / t2 / 1e9 / HBM_PEAK_GBS,
                              "traffic": measured_traffic("C4", B2, "module_net_kernel"),
                              "algorithmic_bytes": round(net_b * B2)},
+                "gather_ceiling": gather_ceiling(lay.module_sizes, B2, t2),
             }
         eng2.close()
 
@@ -330,7 +346,8 @@ def main():
         if l0 > 0:
             kernels["module_net_kernel"] = {
                 "bound": "hbm", "avg_ms": ms0 / l0, "launches": l0,
-                "achieved": net_b * B / (ms0 / l0 / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+                "achieved": net_b * B / (ms0 / l0 / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "gather_ceiling": gather_ceiling(lay.module_sizes, B, ms0 / l0 / 1e3)}
         if meta["with_data"]:
             t1 = ms1 / max(l1, 1) / 1e3
             kernels["module_profile_kernel"] = {
