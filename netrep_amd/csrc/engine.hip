@@ -219,6 +219,15 @@ struct ProfilePlan {
   int64_t basis_doubles = 0;
 };
 
+// Opt-in (NETREP_FUSE=1): measured on C3 the fused kernel takes 24.77 ms per
+// 256-permutation launch against 20.73 + 4.21 ms for the two launches, a 0.7%
+// gain inside run-to-run noise (profiles/r02/profile_variants.txt), so the
+// default keeps the kernels separate and each one's roofline readable.
+bool fuse_enabled() {
+  const char* f = std::getenv("NETREP_FUSE");
+  return f && f[0] == '1';
+}
+
 // The S x S (dual) Gram for modules larger than the sample count; on unless
 // NETREP_DUAL_GRAM=0 (A/B runs).
 bool dual_gram_enabled() {
@@ -466,10 +475,13 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   np.slot_cor_degree = data ? 3 : 2;
   np.slot_avg_cor = data ? 5 : 3;
   np.out = d_out;
-  // The network statistics are their own launch (module_net_kernel) ahead of
-  // the summary-profile kernel; NETREP_CONCURRENT=1 puts them on the side
-  // stream instead.
-  const bool fuse = false;
+  // NETREP_FUSE=1: the network statistics ride in the summary-profile
+  // kernel's item pipeline when every module fits its LDS layout (<= 320
+  // nodes), in the Lanczos vectors' LDS before each item's Gram.
+  // Otherwise (the default: NETREP_FUSE unset) they are their own launch
+  // (module_net_kernel) ahead of the summary-profile kernel;
+  // NETREP_CONCURRENT=1 puts that launch on the side stream.
+  const bool fuse = data && ctx->k_max <= 320 && profile_variant_env() < 0 && fuse_enabled();
   const bool fork = data && !fuse && ctx->concurrent;
   hipStream_t net_stream = fork ? ctx->side : ctx->stream;
   if (fork) {

@@ -105,6 +105,16 @@ __device__ __forceinline__ NetLds carve_net_mem(unsigned char* smem, double* slo
   return L;
 }
 
+// The same layout over a region the caller lends (the summary-profile
+// kernel's Lanczos vectors, idle before its Gram), sharing its index set.
+template <int NW>
+__device__ __forceinline__ NetLds carve_net_over(double* region, double* red, uint32_t* idx, int kmax) {
+  NetLds L = carve_net_lds<NW>(reinterpret_cast<unsigned char*>(region - 8 * NW), kmax);
+  L.red = red;
+  L.idx = idx;
+  return L;
+}
+
 size_t net_lds_bytes(int nw, int kmax) {
   return sizeof(double) * (8 * (size_t)nw + (size_t)(nw + 2) * kmax) + sizeof(unsigned long long) * 3 * (size_t)kmax +
          sizeof(int) * 3 * (size_t)kmax;
@@ -1033,6 +1043,13 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   uint32_t* idx_p = L.idx;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k, kmax,
                        reinterpret_cast<uint32_t*>(gnode + 4 * (int64_t)P.k_max), &idx_p)) {
+    if (P.fuse_net) {
+      // the item's network statistics first (random gathers that overlap the
+      // Gram / Lanczos phases of the co-resident workgroups), in the Lanczos
+      // vectors' LDS, idle until the Gram
+      const NetLds NL = carve_net_over<NW>(L.q, L.red, L.idx, kmax);
+      net_item<NW>(P.net, m, p_local, off, k, NL);
+    }
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     LzLds Li = L;  // this item's view: per-node arrays in scratch when k > kmax
     Li.idx = idx_p;

@@ -163,6 +163,18 @@ def test_c3_nulls_vs_cpp_oracle(c3):
     record("C3 nulls (64 perms x 50 modules, S=500)", max(e1, e2), perms=64)
 
 
+def test_c3_nulls_fused_network_phase(c3, monkeypatch):
+    """The opt-in fused kernel (NETREP_FUSE=1: network statistics inside the
+    summary-profile item loop) gives the same nulls as the separate launches."""
+    seed, p0 = 0x5EED, 5_000
+    base = c3.eng.run(p0, p0 + 32, seed)
+    monkeypatch.setenv("NETREP_FUSE", "1")
+    got = c3.eng.run(p0, p0 + 32, seed)
+    assert_stats_close(got, base, what="C3 fused vs separate")
+    exp, _ = c3.oracle(p0, p0 + 32, seed, True)
+    record("C3 nulls, fused network phase (32 perms)", assert_stats_close(got, exp, what="C3 fused"), perms=32)
+
+
 def test_c4_network_only_full_size(c3):
     """permutationsNoData at 20,000 nodes: 256 permutations x 50 modules."""
     seed, p0 = 77, 9_000
