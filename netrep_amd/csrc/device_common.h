@@ -357,6 +357,14 @@ __device__ __forceinline__ double nr_wave_max(double v) {
   return nr_swap32_max(nr_swap16_max(v));
 }
 
+// Lane l's double, broadcast to the wave (two v_readlane_b32: SGPR result).
+__device__ __forceinline__ double nr_readlane_f64(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 // Transpose-reduce of 16 per-lane column partials up[0..16) over the 64 rows
 // (lanes) of a unit: afterwards lanes with (lane & 3) == 0 hold the column
 // sum of column 8*b5 + 4*b4 + 2*b3 + b2 (b = lane bits). 8 + 4 swaps, 3 + 2

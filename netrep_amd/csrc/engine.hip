@@ -299,7 +299,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
     plan->gram_doubles = 0;  // the Gram lives in registers and LDS
   } else if (variant == 1 || variant == 2) {
     const int64_t kc = plan->k_gram + 1;
-    plan->gram_doubles = (kc * (kc + 1) / 2 + 1 + 31) / 32 * 32;  // packed triangle + zero pad
+    plan->gram_doubles = nr::packed_gram_doubles((int)kc);  // packed triangle in chunked column groups
   } else {
     const int64_t ld = gram_ld(plan->k_gram);
     plan->gram_doubles = ld * ld;

@@ -88,6 +88,8 @@ size_t net_kernel_lds(int k_max);
 bool net_kernel_big(int k_max);        // per-node arrays in global scratch
 size_t net_big_slot_bytes(int k_max);  // global scratch per workgroup in that mode
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant);
+// Doubles of the packed (chunked column-group) Gram of side kc, rounded to 32.
+int64_t packed_gram_doubles(int kc);
 int profile_kvec_max(int m_max);  // longest LDS vectors of the large-module layout (variant 4)
 int reg_kernel_k_max();  // largest module of the register-resident scheme
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);

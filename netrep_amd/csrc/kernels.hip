@@ -509,13 +509,56 @@ __device__ __forceinline__ double reorthogonalise_cgs(const double* __restrict__
 }
 
 
-// Packed symmetric storage: lower triangle, column-major, over kc = k + 1
-// columns (the last is the virtual all-ones column); column c holds rows
-// c .. kc-1 from pk_col(c, kc).
-__device__ __forceinline__ int64_t pk_col(int c, int kc) {
-  return (int64_t)c * kc - (int64_t)c * (c - 1) / 2;
+// Packed symmetric storage of the lower triangle over kc = k + 1 columns (the
+// last is the virtual all-ones column), in chunked column groups: with
+// P = kc rounded up to 16, column group g (columns 16 g .. 16 g + 15) holds
+// rows 16 g .. P - 1 (entries above the diagonal stored as zero, rows and
+// columns >= kc as the zero padding the Gram produces there), cut into row
+// chunks of 64 (the last one h = P - 16 g - 64 j rows); chunk j stores its 16
+// columns one after the other, h rows each. A matvec unit (group, chunk) is
+// then one contiguous run of 16 h doubles, every column piece starting on a
+// 128-byte line (packed_matvec). Group g starts at pk_base(g, P).
+__host__ __device__ __forceinline__ int pk_pad(int kc) { return (kc + 15) & ~15; }
+__host__ __device__ __forceinline__ int64_t pk_base(int g, int P) {
+  return 16 * (int64_t)g * P - 128 * (int64_t)g * (g - 1);
 }
-__device__ __forceinline__ int64_t pk_at(int r, int c, int kc) { return pk_col(c, kc) + (r - c); }
+__device__ __forceinline__ int64_t pk_at(int r, int c, int kc) {  // r >= 16 (c / 16)
+  const int P = pk_pad(kc);
+  const int g = c >> 4;
+  const int rr = r - 16 * g;
+  const int j = rr >> 6;
+  const int h = min(64, P - 16 * g - 64 * j);
+  return pk_base(g, P) + 1024 * (int64_t)j + (int64_t)(c & 15) * h + (rr & 63);
+}
+__device__ __forceinline__ int64_t pk_col(int c, int kc) { return pk_at(c, c, kc); }  // the diagonal G_cc
+
+// Stores one 16 x 16 MFMA accumulator tile of the Gram's super-tile (I2, J2)
+// into the packed layout: lane (i16, kk) holds rows gj = 32 J2 + 16 b + i16 of
+// columns gi = 32 I2 + 16 a + kk + 4 r (f64 MFMA C/D map). The tile lies in
+// one column group (g = 2 I2 + a) and one row chunk, so the chunk, its height
+// and the diagonal test are uniform over it.
+__device__ __forceinline__ void pk_store_tile(double* G, int kc, int I2, int J2, int a, int b,
+                                              const nr_f64x4& v, int lane) {
+  const int P = pk_pad(kc);
+  const int g = 2 * I2 + a;
+  const int rb = 32 * (J2 - I2) + 16 * (b - a);  // first row of the tile, relative to the group's
+  if (rb >= 0 && 16 * g + rb < P) {  // not above the group, nor past the padded side
+    const int j = rb >> 6;
+    const int h = min(64, P - 16 * g - 64 * j);
+    const int i16 = lane & 15, kk = lane >> 4;
+    const int base = (int)pk_base(g, P) + 1024 * j + (rb & 63) + i16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = kk + 4 * r;
+      G[base + t * h] = (rb == 0 && i16 < t) ? 0.0 : v[r];  // zero above the diagonal
+    }
+  }
+}
+
+int64_t packed_gram_doubles(int kc) {
+  const int P = pk_pad(kc);
+  return (pk_base(P / 16, P) + 31) / 32 * 32;
+}
 
 // G = [X 1]^T [X 1] over the k module columns of X (S x N, column-major) plus a
 // virtual all-ones column at index k, so row k of G holds the column sums;
@@ -594,27 +637,26 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
         for (int q = 0; q < 4; ++q) cur[o][q] = full + 4 * kk + q < S ? col[o][full + q] : 0.0;
       mfma16(cur);
     }
-    if (PACKED && t == 0 && lane == 0) G[pk_col(kc, kc)] = 0.0;  // zero pad read by packed_matvec
     const double wgt = (I2 == J2) ? 1.0 : 2.0;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b) {
+        if (PACKED) pk_store_tile(G, kc, I2, J2, a, b, acc[a][b], lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           // D[row = (lane>>4) + 4r][col = lane & 15] (f64 MFMA C/D map)
           const int gi = I2 * 32 + 16 * a + kk + 4 * r;
           const int gj = J2 * 32 + 16 * b + i16;
           const double val = acc[a][b][r];
-          if (PACKED) {
-            if (gi <= gj && gj < kc) G[pk_at(gj, gi, kc)] = val;  // lower triangle, column gi
-          } else {
+          if (!PACKED) {
             G[gi + (int64_t)gj * ld] = val;
             G[gj + (int64_t)gi * ld] = val;
           }
           if (gi < k && gj < k) g1sum += wgt * val;
           if (gi == gj && gi < k) bad |= (int)!isfinite(val);
         }
+      }
   }
 }
 
@@ -674,42 +716,43 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
 #pragma unroll
         for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
     }
-    if (PACKED && t == 0 && lane == 0) G[pk_col(kc, kc)] = 0.0;  // zero pad read by packed_matvec
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b) {
+        if (PACKED) pk_store_tile(G, kc, I2, J2, a, b, acc[a][b], lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int gi = I2 * 32 + 16 * a + kk + 4 * r;
           const int gj = J2 * 32 + 16 * b + i16;
           const double val = acc[a][b][r];
-          if (PACKED) {
-            if (gi <= gj && gj < kc) G[pk_at(gj, gi, kc)] = val;
-          } else {
+          if (!PACKED) {
             G[gi + (int64_t)gj * ld] = val;
             G[gj + (int64_t)gi * ld] = val;
           }
           if (gj == S && gi < S) g1sum += val * val;  // |X 1|^2 from the row sums (X 1)_gi
           if (gi == gj && gi < S) bad |= (int)!isfinite(val);  // H_ss: squares of sample s's values
         }
+      }
   }
 }
 
 // w = G x over the leading k x k block of the PACKED symmetric G (pk_at), NW
-// waves. Work units are (64-row block, 16-column group) pairs with columns
-// c <= last row of the block; lanes own rows. One coalesced read of each
-// column segment feeds the lower part (w_r += G_rc x_c, lane-local) and the
-// mirrored upper part (w_c += sum_{r>c} G_rc x_r), the latter reduced for 16
-// columns at once by the register butterfly above. A unit's 16 loads are
-// issued back to back (no exec-masked lanes: out-of-range lanes read the
-// zero pad element after the triangle), so each wave keeps 16 column
-// segments in flight. Column offsets are wave-uniform (scalar). Per-wave
-// partial arrays keep the sums deterministic. Returns sum_r y_r out_r if y.
+// waves. Work units are (column group, row chunk) pairs, numbered group-major
+// and cut into NW contiguous ranges, one per wave; a unit is one contiguous
+// run of 16 column pieces (16 back-to-back raw buffer loads, lanes own rows,
+// no lane mask except past a short last chunk). Its lower part
+// (w_r += G_rc x_c) is lane-local and added to the wave's row partials; the
+// mirrored upper part (w_c += sum_{r>c} G_rc x_r) accumulates lane-locally
+// over the wave's units of one group and is reduced over the lanes by the
+// register butterfly once per (wave, group). Rows >= k and columns >= k
+// carry x = 0. Per-wave partial arrays keep the sums deterministic. Returns
+// sum_r y_r out_r if y. (tools/probes/matvec_probe.hip: 17-23% faster per
+// pass than row-block units over the plain packed triangle.)
 template <int NW>
-__device__ __forceinline__ double packed_matvec(const double* __restrict__ P, int kc, int k,
-                                                const double* x, double* out, double* part,
-                                                double* upper, int ks, const double* y, double* red) {
+__device__ __forceinline__ double packed_matvec(const double* __restrict__ G, int kc, int k, const double* x,
+                                                 double* out, double* part, double* upper, int ks,
+                                                 const double* y, double* red) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int i = threadIdx.x; i < NW * ks; i += NW * 64) {
@@ -717,42 +760,61 @@ __device__ __forceinline__ double packed_matvec(const double* __restrict__ P, in
     upper[i] = 0.0;
   }
   __syncthreads();
-  // Raw buffer loads: the column offset is a scalar soffset, the row a 32-bit
-  // voffset; out-of-range lanes get voffset 2^31 and the range check returns 0.
-  const int nrec = (kc * (kc + 1) / 2 + 1) * 8;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P, (short)0, nrec, 0x00020000);
-  const int nrb = (k + 63) / 64;
-  for (int rb = 0; rb < nrb; ++rb) {
-    const int r = rb * 64 + lane;
-    const int cmax = min(k, (rb + 1) * 64);
-    const int ncg = (cmax + 15) / 16;
-    const double xr = x[min(r, k - 1)];  // rows >= k carry g = 0
+  const int P = pk_pad(kc);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, (int)(pk_base(P / 16, P) * 8), 0x00020000);
+  const int ncg = (k + 15) / 16;
+  int n_units = 0;
+  for (int g = 0; g < ncg; ++g) n_units += (P - 16 * g + 63) >> 6;
+  const int u0 = n_units * wave / NW, u1 = n_units * (wave + 1) / NW;
+  int cg = 0, first = 0;
+  while (first + ((P - 16 * cg + 63) >> 6) <= u0) {
+    first += (P - 16 * cg + 63) >> 6;
+    ++cg;
+  }
+  int j = u0 - first;
+  int nj = (P - 16 * cg + 63) >> 6;
+  double up[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) up[t] = 0.0;
+  for (int u = u0; u < u1; ++u) {
+    const int c0 = cg * 16;
+    const int L = P - c0;
+    const int h = min(64, L - 64 * j);
+    const int r = c0 + 64 * j + lane;
+    const double xr = r < k ? x[r] : 0.0;
+    const int vo = lane < h ? lane * 8 : (int)0x80000000;
+    int so = (int)(pk_base(cg, P) + 1024 * j) * 8;
+    double g[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      g[t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
+      so += h * 8;
+    }
     double acc = 0.0;
-    for (int cg = wave; cg < ncg; cg += NW) {
-      const int c0 = cg * 16;
-      double g[16];
+    const double xl = c0 + (lane & 15) < k ? x[c0 + (lane & 15)] : 0.0;  // the unit's 16 x_c, one per lane
 #pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const int c = c0 + t;
-        const int colbase = c * kc - c * (c - 1) / 2 - c;  // pk_col(c, kc) - c, scalar
-        const bool ok = c < cmax && r >= c && r < k;
-        g[t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                                              rsrc, ok ? r * 8 : (int)0x80000000, colbase * 8, 0));
-      }
+    for (int t = 0; t < 16; ++t) acc += g[t] * nr_readlane_f64(xl, t);  // (saves 30 VGPRs over 16 LDS reads)
+    if (j > 0) {
 #pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const int c = c0 + t;
-        acc += g[t] * x[min(c, k - 1)];  // columns >= cmax carry g = 0
-        g[t] = (r > c) ? g[t] * xr : 0.0;  // in place: upper-part partials
-      }
-      const double v = nr_transpose_reduce16(g, lane);
-      if ((lane & 3) == 0) {
-        const int c = c0 + ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 +
-                      ((lane >> 2) & 1);
-        if (c < cmax) upper[wave * ks + c] += v;
-      }
+      for (int t = 0; t < 16; ++t) up[t] += g[t] * xr;
+    } else {  // the chunk holding the group's diagonal block
+#pragma unroll
+      for (int t = 0; t < 16; ++t) up[t] += (r > c0 + t) ? g[t] * xr : 0.0;
     }
     if (r < k) part[wave * ks + r] += acc;
+    ++j;
+    if (j == nj || u + 1 == u1) {
+      const double v = nr_transpose_reduce16(up, lane);
+      if ((lane & 3) == 0) {
+        const int c = c0 + ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+        if (c < k) upper[wave * ks + c] += v;
+      }
+#pragma unroll
+      for (int t = 0; t < 16; ++t) up[t] = 0.0;
+      ++cg;
+      j = 0;
+      nj = (P - 16 * cg + 63) >> 6;
+    }
   }
   __syncthreads();
   double d[1] = {0.0};
