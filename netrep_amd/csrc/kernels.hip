@@ -746,20 +746,16 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
 // mirrored upper part (w_c += sum_{r>c} G_rc x_r) accumulates lane-locally
 // over the wave's units of one group and is reduced over the lanes by the
 // register butterfly once per (wave, group). Rows >= k and columns >= k
-// carry x = 0. Per-wave partial arrays keep the sums deterministic. Returns
-// sum_r y_r out_r if y. (tools/probes/matvec_probe.hip: 17-23% faster per
-// pass than row-block units over the plain packed triangle.)
+// carry x = 0. Per-wave partial arrays keep the sums deterministic; they are
+// zero on entry (zeroed once per kernel and again by the combine that reads
+// them). Returns sum_r y_r out_r if y. (tools/probes/matvec_probe.hip: 17-23%
+// faster per pass than row-block units over the plain packed triangle.)
 template <int NW>
 __device__ __forceinline__ double packed_matvec(const double* __restrict__ G, int kc, int k, const double* x,
                                                  double* out, double* part, double* upper, int ks,
                                                  const double* y, double* red) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int i = threadIdx.x; i < NW * ks; i += NW * 64) {
-    part[i] = 0.0;
-    upper[i] = 0.0;
-  }
-  __syncthreads();
   const int P = pk_pad(kc);
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, (int)(pk_base(P / 16, P) * 8), 0x00020000);
   const int ncg = (k + 15) / 16;
@@ -821,7 +817,11 @@ __device__ __forceinline__ double packed_matvec(const double* __restrict__ G, in
   for (int rr = threadIdx.x; rr < k; rr += NW * 64) {
     double sum = 0.0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) sum += part[w * ks + rr] + upper[w * ks + rr];
+    for (int w = 0; w < NW; ++w) {
+      sum += part[w * ks + rr] + upper[w * ks + rr];
+      part[w * ks + rr] = 0.0;  // zero again for the next matvec (block_sums' barriers order it)
+      upper[w * ks + rr] = 0.0;
+    }
     out[rr] = sum;
     if (y) d[0] += y[rr] * sum;
   }
@@ -1100,6 +1100,10 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   const double* __restrict__ X = P.data;
   const double Sd = (double)S;
 
+  if (PACKED) {  // the matvec's partial arrays start zero (packed_matvec keeps them so)
+    for (int i = tid; i < 2 * NW * kmax; i += BS) part[i] = 0.0;
+    __syncthreads();
+  }
   int m, k;
   int64_t p_local, off;
   uint32_t* idx_p = L.idx;
@@ -1111,6 +1115,8 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       // vectors' LDS, idle until the Gram
       const NetLds NL = carve_net_over<NW>(L.q, L.red, L.idx, kmax);
       net_item<NW>(P.net, m, p_local, off, k, NL);
+      if (PACKED)  // its arrays overlap the matvec partials
+        for (int i = tid; i < 2 * NW * kmax; i += BS) part[i] = 0.0;
     }
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     LzLds Li = L;  // this item's view: per-node arrays in scratch when k > kmax
