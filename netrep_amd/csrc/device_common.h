@@ -635,8 +635,19 @@ __device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L
   const int item = flags[0];
   __syncthreads();
   if (item >= P.n_items) return false;
-  const int64_t mslot = item / P.n_perm;
-  p_local = item - mslot * P.n_perm;
+  int64_t mslot;
+  const int T = P.order_tail;
+  const int64_t n_ms = P.n_items / P.n_perm;
+  const int64_t head = T > 0 && T < P.n_perm ? (int64_t)(P.n_perm - T) * n_ms : 0;
+  if (item < head) {  // permutation-major: every module size in flight at once
+    p_local = item / n_ms;
+    mslot = item - p_local * n_ms;
+  } else {            // module-major, large modules first (the tail balances the slots)
+    const int64_t t = item - head;
+    const int64_t np = head > 0 ? T : P.n_perm;
+    mslot = t / np;
+    p_local = (P.n_perm - np) + (t - mslot * np);
+  }
   m = P.mod_order[mslot];
   off = P.node_off[m];
   k = (int)(P.node_off[m + 1] - off);

@@ -243,6 +243,22 @@ int profile_variant_env() {
   return v == "packed" ? 1 : v == "full" ? 0 : v == "reg" ? 3 : v == "packed4" ? 2 : v == "rg4" ? 5 : -1;
 }
 
+// Queue order of the summary-profile items. Module-major (every permutation
+// of the largest module, then the next) keeps the largest Grams in flight
+// together: at C3 the 768 slots' first items (modules of 289-300 nodes, a
+// ~350 KB packed Gram plus its Lanczos basis each) overflow the 256 MiB
+// Infinity Cache, so their matvecs stream from HBM. Permutation-major order
+// keeps the size mix of the whole launch in flight; its last T permutations
+// (about one slot's worth of items) run module-major, largest first, so the
+// slots still drain together. NETREP_PROFILE_ORDER_TAIL=0 restores
+// module-major order (A/B runs); any other value fixes T.
+int profile_order_tail(int slots, int n_mod, int64_t n_perm) {
+  if (const char* e = std::getenv("NETREP_PROFILE_ORDER_TAIL")) return std::max(0, std::atoi(e));
+  if (n_mod <= 1) return 0;
+  const int64_t t = (slots + n_mod - 1) / n_mod;
+  return t >= n_perm ? 0 : (int)t;
+}
+
 // rg4: plan the register-resident 4-wave kernel (variant 5; the caller
 // guarantees k_max <= rg4_kernel_k_max()).
 int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg4, ProfilePlan* plan) {
@@ -355,6 +371,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.scratch = ctx->d_scratch;
     pp.scratch_stride = plan.stride;
     pp.part_global = plan.variant == 4 ? 1 : 0;
+    pp.order_tail = profile_order_tail(plan.slots, seg[i].count, n_perm);
     NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
     if (plan.variant == 5)
       NR_HIP(ctx, nr::launch_profile_rg4(pp, plan.slots, st));

@@ -81,6 +81,9 @@ struct ProfileParams {
   int32_t kvec;                // LDS vector length (0: k_max); larger (dual) modules keep their
                                // per-node arrays in the slot's scratch
   int64_t basis_doubles;       // Lanczos basis doubles per slot (behind the Gram)
+  int32_t order_tail;          // queue order: 0 = module-major (large modules first); T > 0 =
+                               // permutation-major over all modules (a size mix in flight) for the
+                               // first n_perm - T permutations, the last T module-major
   NetParams net;
 };
 
