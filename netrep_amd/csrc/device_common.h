@@ -418,6 +418,13 @@ __device__ __forceinline__ double rg_row_reduce(const double (&a)[4], int lane) 
 // the persistent work queue.
 // ---------------------------------------------------------------------------
 
+// Doubles of the packed matvec's per-wave partial arrays, which double as the
+// Ritz checks' work area (5 mmax).
+__host__ __device__ __forceinline__ int64_t packed_part_doubles(int nw, int kvec, int mmax) {
+  const int64_t a = (int64_t)nw * kvec, b = 5 * (int64_t)mmax;
+  return a > b ? a : b;
+}
+
 // LDS carve-out common to all summary-profile bodies.
 struct LzLds {
   double *red, *q, *qprev, *w, *vv, *gv, *colm;
@@ -431,7 +438,7 @@ struct LzLds {
 // arrays and idx. Layout matches profile_kernel_lds / reg_kernel_lds.
 template <int NW>
 __device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mmax, int64_t extra,
-                                           double** extra_out) {
+                                           double** extra_out, bool twork_in_extra = false) {
   LzLds L;
   L.red = reinterpret_cast<double*>(smem);  // 8 * NW
   L.q = L.red + 8 * NW;
@@ -445,8 +452,10 @@ __device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mm
   L.beta = L.alpha + mmax;       // [mmax]
   L.h = L.beta + mmax;           // [mmax]
   L.ty = L.h + mmax;             // [mmax]
-  L.twork = L.ty + mmax;         // [5 * mmax]
-  L.omg = L.twork + 5 * mmax;    // [3 * (mmax + 1)] omega rows
+  // [5 * mmax]; or the extra area (the packed matvec's partials, idle and zero
+  // between matvecs: users zero it again)
+  L.twork = twork_in_extra ? *extra_out : L.ty + mmax;
+  L.omg = twork_in_extra ? L.ty + mmax : L.twork + 5 * mmax;  // [3 * (mmax + 1)] omega rows
   L.idx = reinterpret_cast<uint32_t*>(L.omg + 3 * (mmax + 1));  // [kvec]
   L.mmax = mmax;
   return L;

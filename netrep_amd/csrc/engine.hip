@@ -217,6 +217,7 @@ struct ProfilePlan {
   int kvec = 0;       // LDS vector length
   bool big = false;   // modules beyond kvec (per-node arrays in scratch)
   int64_t basis_doubles = 0;
+  int64_t g32_off = 0;  // fp32 Gram copy (relaxed Lanczos steps), 0: none
 };
 
 // Opt-in (NETREP_FUSE=1): measured on C3 the fused kernel takes 24.77 ms per
@@ -232,6 +233,13 @@ bool fuse_enabled() {
 // NETREP_DUAL_GRAM=0 (A/B runs).
 bool dual_gram_enabled() {
   const char* f = std::getenv("NETREP_DUAL_GRAM");
+  return !(f && f[0] == '0');
+}
+
+// Relaxed Lanczos steps on an fp32 copy of the packed Gram once the residual
+// is below 1e-7 theta (kernels.hip lanczos_ritz); on unless NETREP_RELAX=0.
+bool relax_enabled() {
+  const char* f = std::getenv("NETREP_RELAX");
   return !(f && f[0] == '0');
 }
 
@@ -303,7 +311,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
   if (lds > 160 * 1024)
     return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
   int want = variant == 1 ? 2 : 3;
-  if (const char* e = std::getenv("NETREP_PROFILE_WG_PER_CU")) want = std::max(1, std::min(3, std::atoi(e)));
+  if (const char* e = std::getenv("NETREP_PROFILE_WG_PER_CU")) want = std::max(1, std::min(4, std::atoi(e)));
   if (variant == 1) want = std::min(want, 2);
   if (variant == 2) want = std::max(2, want);
   if (variant == 3 || variant == 4) want = 1;
@@ -324,6 +332,12 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
   plan->stride = plan->gram_doubles + plan->basis_doubles +
                  (variant == 4 ? (int64_t)nr::kProfileWaves * kvec : 0) +
                  (plan->big ? 5 * (int64_t)k_max : 0);  // x.u, means, squares, contributions, index set
+  plan->g32_off = 0;
+  if ((variant == 1 || variant == 2) && relax_enabled()) {  // fp32 copy of the packed Gram at the slot's end
+    plan->stride = (plan->stride + 31) / 32 * 32;
+    plan->g32_off = plan->stride;
+    plan->stride += (plan->gram_doubles / 2 + 31) / 32 * 32;
+  }
   return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
 }
 
@@ -372,6 +386,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.scratch_stride = plan.stride;
     pp.part_global = plan.variant == 4 ? 1 : 0;
     pp.order_tail = profile_order_tail(plan.slots, seg[i].count, n_perm);
+    pp.g32_off = plan.variant == 5 ? 0 : plan.g32_off;
     NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
     if (plan.variant == 5)
       NR_HIP(ctx, nr::launch_profile_rg4(pp, plan.slots, st));

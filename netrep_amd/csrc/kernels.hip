@@ -537,7 +537,7 @@ __device__ __forceinline__ int64_t pk_col(int c, int kc) { return pk_at(c, c, kc
 // columns gi = 32 I2 + 16 a + kk + 4 r (f64 MFMA C/D map). The tile lies in
 // one column group (g = 2 I2 + a) and one row chunk, so the chunk, its height
 // and the diagonal test are uniform over it.
-__device__ __forceinline__ void pk_store_tile(double* G, int kc, int I2, int J2, int a, int b,
+__device__ __forceinline__ void pk_store_tile(double* G, float* G32, int kc, int I2, int J2, int a, int b,
                                               const nr_f64x4& v, int lane) {
   const int P = pk_pad(kc);
   const int g = 2 * I2 + a;
@@ -550,7 +550,9 @@ __device__ __forceinline__ void pk_store_tile(double* G, int kc, int I2, int J2,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int t = kk + 4 * r;
-      G[base + t * h] = (rb == 0 && i16 < t) ? 0.0 : v[r];  // zero above the diagonal
+      const double x = (rb == 0 && i16 < t) ? 0.0 : v[r];  // zero above the diagonal
+      G[base + t * h] = x;
+      if (G32) G32[base + t * h] = (float)x;  // the relaxed-phase copy (packed_matvec<NW, true>)
     }
   }
 }
@@ -576,7 +578,7 @@ int64_t packed_gram_doubles(int kc) {
 // non-finite flag.
 template <int NW = NR_WAVES, bool PACKED = false>
 __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* idx, int k, int64_t ones_off,
-                          double* __restrict__ G, int ld, double& g1sum, int& bad) {
+                          double* __restrict__ G, float* __restrict__ G32, int ld, double& g1sum, int& bad) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, kk = lane >> 4;
   const int kc = k + 1;
@@ -642,7 +644,7 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        if (PACKED) pk_store_tile(G, kc, I2, J2, a, b, acc[a][b], lane);
+        if (PACKED) pk_store_tile(G, G32, kc, I2, J2, a, b, acc[a][b], lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           // D[row = (lane>>4) + 4r][col = lane & 15] (f64 MFMA C/D map)
@@ -674,7 +676,7 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
 // (from H's diagonal).
 template <int NW = NR_WAVES, bool PACKED = false>
 __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32_t* idx, int k,
-                               double* __restrict__ G, int ld, double& g1sum, int& bad) {
+                               double* __restrict__ G, float* __restrict__ G32, int ld, double& g1sum, int& bad) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, kk = lane >> 4;
   const int kc = S + 1;
@@ -720,7 +722,7 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        if (PACKED) pk_store_tile(G, kc, I2, J2, a, b, acc[a][b], lane);
+        if (PACKED) pk_store_tile(G, G32, kc, I2, J2, a, b, acc[a][b], lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int gi = I2 * 32 + 16 * a + kk + 4 * r;
@@ -746,18 +748,24 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
 // mirrored upper part (w_c += sum_{r>c} G_rc x_r) accumulates lane-locally
 // over the wave's units of one group and is reduced over the lanes by the
 // register butterfly once per (wave, group). Rows >= k and columns >= k
-// carry x = 0. Per-wave partial arrays keep the sums deterministic; they are
-// zero on entry (zeroed once per kernel and again by the combine that reads
-// them). Returns sum_r y_r out_r if y. (tools/probes/matvec_probe.hip: 17-23%
+// carry x = 0. Both parts go to the wave's one partial array (the wave's own
+// LDS operations are ordered), and per-wave arrays keep the sums
+// deterministic; they are zero on entry (zeroed once per kernel and again by
+// the combine that reads them). Returns sum_r y_r out_r if y. (tools/probes/matvec_probe.hip: 17-23%
 // faster per pass than row-block units over the plain packed triangle.)
-template <int NW>
-__device__ __forceinline__ double packed_matvec(const double* __restrict__ G, int kc, int k, const double* x,
-                                                 double* out, double* part, double* upper, int ks,
+//
+// F32: the same matvec over the fp32 copy of G (G32, same packed indexing),
+// the Lanczos steps after the residual has dropped below 1e-7 theta
+// (lanczos_ritz): half the bytes per pass, fp64 arithmetic.
+template <int NW, bool F32 = false>
+__device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int kc, int k, const double* x,
+                                                 double* out, double* part, int ks,
                                                  const double* y, double* red) {
+  constexpr int EB = F32 ? 4 : 8;  // element bytes
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = pk_pad(kc);
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, (int)(pk_base(P / 16, P) * 8), 0x00020000);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, (int)(pk_base(P / 16, P) * EB), 0x00020000);
   const int ncg = (k + 15) / 16;
   int n_units = 0;
   for (int g = 0; g < ncg; ++g) n_units += (P - 16 * g + 63) >> 6;
@@ -778,13 +786,16 @@ __device__ __forceinline__ double packed_matvec(const double* __restrict__ G, in
     const int h = min(64, L - 64 * j);
     const int r = c0 + 64 * j + lane;
     const double xr = r < k ? x[r] : 0.0;
-    const int vo = lane < h ? lane * 8 : (int)0x80000000;
-    int so = (int)(pk_base(cg, P) + 1024 * j) * 8;
+    const int vo = lane < h ? lane * EB : (int)0x80000000;
+    int so = (int)(pk_base(cg, P) + 1024 * j) * EB;
     double g[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      g[t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
-      so += h * 8;
+      if (F32)
+        g[t] = (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo, so, 0));
+      else
+        g[t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
+      so += h * EB;
     }
     double acc = 0.0;
     const double xl = c0 + (lane & 15) < k ? x[c0 + (lane & 15)] : 0.0;  // the unit's 16 x_c, one per lane
@@ -803,7 +814,7 @@ __device__ __forceinline__ double packed_matvec(const double* __restrict__ G, in
       const double v = nr_transpose_reduce16(up, lane);
       if ((lane & 3) == 0) {
         const int c = c0 + ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
-        if (c < k) upper[wave * ks + c] += v;
+        if (c < k) part[wave * ks + c] += v;
       }
 #pragma unroll
       for (int t = 0; t < 16; ++t) up[t] = 0.0;
@@ -818,9 +829,8 @@ __device__ __forceinline__ double packed_matvec(const double* __restrict__ G, in
     double sum = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      sum += part[w * ks + rr] + upper[w * ks + rr];
+      sum += part[w * ks + rr];
       part[w * ks + rr] = 0.0;  // zero again for the next matvec (block_sums' barriers order it)
-      upper[w * ks + rr] = 0.0;
     }
     out[rr] = sum;
     if (y) d[0] += y[rr] * sum;
@@ -913,9 +923,15 @@ __device__ __forceinline__ double reorthogonalise_bf(const double* __restrict__ 
 // (one CGS pass against the basis Q, k x mcap in global scratch), top Ritz
 // pair of the tridiagonal by Sturm multisection + inverse iteration at
 // predicted convergence checks. Leaves the normalised Ritz vector in L.vv.
+// relax (optional): set from the first check whose residual is below
+// 1e-7 theta on; the caller's mv then reads the fp32 copy of G. Matvec errors
+// that late no longer move the converged Ritz vector (relaxed Krylov
+// accuracy: the later a step, the smaller its weight in the Ritz vector;
+// offline study on C3 null items, tools/sim_lanczos_relax.py: same steps, same
+// 2e-14 worst eigenvector error as fp64 throughout, 19% fewer Gram bytes).
 template <int NW, bool BF, class MV>
 __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, const LzLds& L, int* flags,
-                                             double* Q, MV& mv, uint64_t& t_mark) {
+                                             double* Q, MV& mv, uint64_t& t_mark, bool* relax = nullptr) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mmax = L.mmax;
@@ -965,6 +981,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   if (tid == 0) {
     omg[0] = 1.0;  // omega_{0,0}
     s_reorth = 0;
+    flags[5] = 0;  // relaxed (fp32) matvecs
   }
   for (int j = 0; j < mcap; ++j) {
     for (int c = tid; c < k; c += BS) Q[(int64_t)j * k + c] = q[c];
@@ -987,6 +1004,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     if (s_reorth) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
       nb = BF ? reorthogonalise_bf<NW>(Q, k, j + 1, w, h, twork, 5 * mmax, red)  // twork idle until the next check
               : reorthogonalise_cgs<NW>(Q, k, j + 1, w, h, red);
+      if (BF) {  // twork is the packed matvec's partial array: zero again
+        for (int i = tid; i < 5 * mmax; i += BS) twork[i] = 0.0;
+        __syncthreads();
+      }
       alpha_j += h[j];
       if (wave == 0) {
         const double eps = 2.220446049250313e-16;
@@ -1014,6 +1035,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
           const double tol = 5e-15 * fabs(theta);
           const bool conv = resid <= tol;
           s_done = conv || last || !(beta_j > 1e-300 * fabs(theta));
+          if (relax && resid <= 1e-7 * fabs(theta)) flags[5] = 1;
           // the Ritz vector's coefficients: inverse iteration (LU), once
           if (s_done) tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
           if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
@@ -1031,6 +1053,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       __syncthreads();
       if (s_done) break;
       next_check = s_next_check;
+      if (relax) *relax = flags[5] != 0;
     }
     const double inv = 1.0 / beta_j;
     for (int c = tid; c < k; c += BS) {
@@ -1053,6 +1076,8 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     L.vv[c] = s;
     nv[0] += s * s;
   }
+  if (BF)  // twork (the packed matvec's partials) held the tridiagonal LU: zero again
+    for (int i = tid; i < 5 * mmax; i += BS) twork[i] = 0.0;
   block_sums<1, NW>(nv, red);
   {
     const double inv = 1.0 / sqrt(nv[0]);
@@ -1086,13 +1111,17 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   // in the slot's scratch behind the basis; the workgroup's barriers order
   // them (one CU, one vector L1).
   const bool pglob = !PACKED && P.part_global;
-  const LzLds L = carve_lds<NW>(smem, kmax, mmax, pglob ? 0 : (int64_t)(PACKED ? 2 : 1) * NW * kmax, &part);
+  // packed: one partial array per wave, which also serves as the Ritz checks'
+  // work area (twork, 5 mmax doubles) between matvecs
+  const int64_t n_part = PACKED ? packed_part_doubles(NW, kmax, mmax) : (int64_t)NW * kmax;
+  const LzLds L = carve_lds<NW>(smem, kmax, mmax, pglob ? 0 : n_part, &part, PACKED);
   const int tid = threadIdx.x;
   double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;  // Gram
   const int ld = P.ld;
   double* Q = G + P.gram_doubles;                                  // Lanczos basis
+  // fp32 copy of the packed Gram for the relaxed Lanczos steps (0: off)
+  float* G32 = PACKED && P.g32_off > 0 ? reinterpret_cast<float*>(G + P.g32_off) : nullptr;
   if (pglob) part = Q + P.basis_doubles;
-  double* upper = part + NW * kmax;  // packed only
   // modules of more than kmax nodes (dual by construction, engine.hip
   // plan_profile): x_c.u, column means, sums of squares, contributions and the
   // index set in the slot's scratch
@@ -1101,7 +1130,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   const double Sd = (double)S;
 
   if (PACKED) {  // the matvec's partial arrays start zero (packed_matvec keeps them so)
-    for (int i = tid; i < 2 * NW * kmax; i += BS) part[i] = 0.0;
+    for (int i = tid; i < n_part; i += BS) part[i] = 0.0;
     __syncthreads();
   }
   int m, k;
@@ -1116,7 +1145,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       const NetLds NL = carve_net_over<NW>(L.q, L.red, L.idx, kmax);
       net_item<NW>(P.net, m, p_local, off, k, NL);
       if (PACKED)  // its arrays overlap the matvec partials
-        for (int i = tid; i < 2 * NW * kmax; i += BS) part[i] = 0.0;
+        for (int i = tid; i < n_part; i += BS) part[i] = 0.0;
     }
     NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
     LzLds Li = L;  // this item's view: per-node arrays in scratch when k > kmax
@@ -1134,9 +1163,9 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     double g1[1] = {0.0};
     int bad = 0;
     if (dual)
-      gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, ld, g1[0], bad);
+      gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
     else
-      gram_mfma<NW, PACKED>(X, S, L.idx, k, P.ones_off, G, ld, g1[0], bad);
+      gram_mfma<NW, PACKED>(X, S, L.idx, k, P.ones_off, G, G32, ld, g1[0], bad);
     if (bad) atomicOr(&s_flags[1], 1);
     block_sums<1, NW>(g1, L.red);  // barriers also publish G to the whole workgroup
     NR_STAMP(1);  // Gram
@@ -1144,11 +1173,14 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       if (!dual)
         for (int c = tid; c < k; c += BS)
           L.colm[c] = (PACKED ? G[pk_at(k, c, kc)] : G[k + (int64_t)c * ld]) / Sd;
+      bool relax = false;
       auto mv = [&](const double* x, double* out, const double* y) -> double {
-        return PACKED ? packed_matvec<NW>(G, kc, n, x, out, part, upper, kmax, y, L.red)
-                      : matvec(G, ld, n, x, out, part, kmax, y, L.red);
+        if (!PACKED) return matvec(G, ld, n, x, out, part, kmax, y, L.red);
+        return relax ? packed_matvec<NW, true>(G32, kc, n, x, out, part, kmax, y, L.red)
+                     : packed_matvec<NW>(G, kc, n, x, out, part, kmax, y, L.red);
       };
-      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark);
+      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr);
+      relax = false;  // node contributions: the fp64 Gram
       if (dual) {
         profile_contrib_dual<NW>(P, k, m, Li, X, S, g1[0]);
       } else {
@@ -1712,7 +1744,10 @@ size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
     k_max = packed_bucket(k_max);
     m_max = k_max < 160 ? k_max : 160;
   }
-  return sizeof(double) * (8 * nw + (6 + (packed ? 2 : 1) * nw) * (size_t)k_max + 12 * (size_t)m_max + 3) +
+  if (packed)  // the partials double as twork (packed_part_doubles)
+    return sizeof(double) * (8 * nw + 6 * (size_t)k_max + packed_part_doubles(nw, k_max, m_max) + 7 * (size_t)m_max + 3) +
+           sizeof(uint32_t) * k_max;
+  return sizeof(double) * (8 * nw + (6 + (size_t)nw) * (size_t)k_max + 12 * (size_t)m_max + 3) +
          sizeof(uint32_t) * k_max;
 }
 
@@ -1744,7 +1779,9 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
     return hipGetLastError();
   }
   if (variant == 2) {
-    if (b320 && wg_per_cu >= 3)
+    if (b320 && wg_per_cu >= 4)
+      hipLaunchKernelGGL((module_profile_packed4_kernel<320, 4>), g, b4, lds, st, P);
+    else if (b320 && wg_per_cu >= 3)
       hipLaunchKernelGGL((module_profile_packed4_kernel<320, 3>), g, b4, lds, st, P);
     else if (b320)
       hipLaunchKernelGGL((module_profile_packed4_kernel<320, 2>), g, b4, lds, st, P);

@@ -472,7 +472,7 @@ __global__ void __launch_bounds__(256, 3) mv_probe(double* Gall, int64_t stride,
       for (int c = threadIdx.x; c < k; c += 256) w[c] = x[c];
       __syncthreads();
     } else {
-      lam = V == 0 ? packed_matvec<NW>(G, k + 1, k, x, w, part, upper, KS, x, red)
+      lam = V == 0 ? packed_matvec<NW>(G, k + 1, k, x, w, part, KS, x, red)
                    : packed_matvec_pipe<NW>(G, k + 1, k, x, w, part, upper, KS, x, red);
     }
     const double inv = 1.0 / fabs(lam);

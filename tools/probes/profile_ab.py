@@ -44,7 +44,12 @@ def main():
     ref = None
     flops = (2.0 * n_samples * k.astype(np.float64) ** 2).sum() * 256
     for v in variants:
-        os.environ["NETREP_PROFILE_VARIANT"] = v
+        # "name:ENV=VAL,ENV=VAL" sets engine knobs for this variant only
+        name, _, knobs = v.partition(":")
+        os.environ["NETREP_PROFILE_VARIANT"] = name
+        for kv in [x for x in knobs.split(",") if x]:
+            key, _, val = kv.partition("=")
+            os.environ[key] = val
         eng.run(0, 256, 7)
         eng.synchronize()
         eng.set_timing(True)
@@ -75,6 +80,8 @@ def main():
         per_item = {kk: round(vv / (512 * n_mod)) for kk, vv in st.items() if vv}
         print(f"   stamps {frac}")
         print(f"   wave-0 cycles per item {per_item}")
+        for kv in [x for x in knobs.split(",") if x]:
+            os.environ.pop(kv.partition("=")[0], None)
 
 
 if __name__ == "__main__":
