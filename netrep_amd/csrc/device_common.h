@@ -30,8 +30,9 @@ __device__ __forceinline__ double nr_wave_max(double v);
 __device__ __forceinline__ double wave_sum(double v) { return nr_wave_sum(v); }
 
 // Block-wide sums of N values; result broadcast to every thread. `red` must
-// hold N * NR_WAVES doubles of LDS. Contains two barriers.
-template <int N, int NW = NR_WAVES>
+// hold N * NR_WAVES doubles of LDS. Contains two barriers (one with
+// TRAIL = false: then `red` must not be written again before a later barrier).
+template <int N, int NW = NR_WAVES, bool TRAIL = true>
 __device__ __forceinline__ void block_sums(double (&v)[N], double* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -48,7 +49,7 @@ __device__ __forceinline__ void block_sums(double (&v)[N], double* red) {
     for (int w = 0; w < NW; ++w) s += red[i * NW + w];
     v[i] = s;
   }
-  __syncthreads();
+  if (TRAIL) __syncthreads();
 }
 
 // Pearson correlation from (shifted) one-pass sums over complete cases.
@@ -280,14 +281,15 @@ static __device__ __forceinline__ void tri_eigenvector(const double* alpha, cons
 // Partial reorthogonalisation (Simon 1984): omega_{j+1,i} estimates q_{j+1}.q_i
 // from the recurrence on T's entries; run by one wave over i = 0..j. Returns
 // max_i |omega_{j+1,i}| (all lanes). om_cur = omega_{j,.}, om_prev = omega_{j-1,.}.
-__device__ __forceinline__ double omega_update(const double* alpha, const double* beta, int j, double beta_j,
+__device__ __forceinline__ double omega_update(const double* alpha, const double* beta, int j, double alpha_j,
+                                               double beta_j,
                                                const double* om_cur, const double* om_prev, double* om_next,
                                                double anorm, int k, int lane) {
   const double eps = 2.220446049250313e-16;
   const double psi = eps * anorm / beta_j;
   double mx = 0.0;
   for (int i = lane; i < j; i += 64) {
-    double t = beta[i] * om_cur[i + 1] + (alpha[i] - alpha[j]) * om_cur[i] -
+    double t = beta[i] * om_cur[i + 1] + (alpha[i] - alpha_j) * om_cur[i] -
                (j > 0 ? beta[j - 1] * om_prev[i] : 0.0);
     if (i > 0) t += beta[i - 1] * om_cur[i - 1];
     t = t / beta_j;

@@ -455,7 +455,8 @@ __device__ __forceinline__ double matvec(const double* __restrict__ G, int ld, i
   return d[0];
 }
 
-// Lanczos 3-term step w <- w - a q - b qprev; returns |w|^2.
+// Lanczos 3-term step w <- w - a q - b qprev; returns |w|^2. No trailing
+// barrier: `red` must not be written again before the next barrier.
 template <int NW = NR_WAVES>
 __device__ __forceinline__ double three_term(int k, double* w, const double* q, const double* qprev,
                                              double a, double b, double* red) {
@@ -465,7 +466,7 @@ __device__ __forceinline__ double three_term(int k, double* w, const double* q, 
     w[c] = z;
     nrm[0] += z * z;
   }
-  block_sums<1, NW>(nrm, red);
+  block_sums<1, NW, false>(nrm, red);
   return nrm[0];
 }
 
@@ -835,7 +836,10 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
     out[rr] = sum;
     if (y) d[0] += y[rr] * sum;
   }
-  block_sums<1, NW>(d, red);
+  // y . out, without the trailing barrier (the caller's next writer of `red`
+  // is behind a barrier); no y: each thread reads back only its own out[]
+  // entries before the caller's next barrier
+  if (y) block_sums<1, NW, false>(d, red);
   return d[0];
 }
 
@@ -986,18 +990,20 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   for (int j = 0; j < mcap; ++j) {
     for (int c = tid; c < k; c += BS) Q[(int64_t)j * k + c] = q[c];
     NR_STAMP(2);  // Lanczos: vector updates / tridiagonal checks
+    // Barriers per step: the matvec's combine and its sum, the 3-term norm,
+    // the omega decision, and one after the q update (+ one per check). The
+    // two block sums write alternate halves of `red` and skip their trailing
+    // barrier: the next writer of each half is behind the omega barrier.
     const double alpha0 = mv(q, w, q);
     NR_STAMP(3);  // Lanczos: matvec
-    double nb = three_term<NW>(k, w, q, qprev, alpha0, beta_prev, red);
+    double nb = three_term<NW>(k, w, q, qprev, alpha0, beta_prev, red + NW);
     double alpha_j = alpha0;
     double* om_cur = omg + (j % 3) * (mmax + 1);
     double* om_prev = omg + ((j + 2) % 3) * (mmax + 1);
     double* om_next = omg + ((j + 1) % 3) * (mmax + 1);
     anorm = fmax(anorm, fabs(alpha0) + sqrt(nb) + beta_prev);
-    if (tid == 0) alpha[j] = alpha0;
-    __syncthreads();
-    if (wave == 0) {
-      const double mx = omega_update(alpha, beta, j, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
+    if (wave == 0) {  // alpha[j] passed in registers: no barrier before the recurrence
+      const double mx = omega_update(alpha, beta, j, alpha0, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
       if (lane == 0) s_reorth = force_next || mx > sqrt_eps;
     }
     __syncthreads();
@@ -1023,7 +1029,16 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       beta[j] = beta_j;
     }
     nsteps = j + 1;
+    {  // next Lanczos vector (unused if this step's check ends the run)
+      const double inv = 1.0 / beta_j;
+      for (int c = tid; c < k; c += BS) {
+        qprev[c] = q[c];
+        q[c] = w[c] * inv;
+      }
+    }
+    beta_prev = beta_j;
     __syncthreads();
+    NR_STAMP(6);  // Lanczos: q update + barrier
     const bool last = (j + 1 == mcap);
     if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
       if (wave == 0) {
@@ -1054,14 +1069,8 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       if (s_done) break;
       next_check = s_next_check;
       if (relax) *relax = flags[5] != 0;
+      NR_STAMP(7);  // Lanczos: Ritz checks
     }
-    const double inv = 1.0 / beta_j;
-    for (int c = tid; c < k; c += BS) {
-      qprev[c] = q[c];
-      q[c] = w[c] * inv;
-    }
-    beta_prev = beta_j;
-    __syncthreads();
   }
   NR_STAMP(2);
   if (tid == 0 && P.diag) {

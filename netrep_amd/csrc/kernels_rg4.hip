@@ -511,7 +511,7 @@ __device__ __forceinline__ void r4_lanczos(const ProfileParams& P, int k, int kp
     double* om_cur = omg + (j % 3) * (R4_MCAP + 1);
     double* om_prev = omg + ((j + 2) % 3) * (R4_MCAP + 1);
     double* om_next = omg + ((j + 1) % 3) * (R4_MCAP + 1);
-    const double mx = omega_update(L.alpha, L.beta, j, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
+    const double mx = omega_update(L.alpha, L.beta, j, L.alpha[j], sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
     const bool reorth = force_next || mx > sqrt_eps;
     if (reorth) {
       NR_STAMP(7);

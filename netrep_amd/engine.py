@@ -247,7 +247,7 @@ class Engine:
     def stamps(self):
         out = (C.c_uint64 * 8)()
         self._check(self._lib.nr_get_stamps(self._h, out))
-        names = ["index", "gram", "lanczos_vec", "lanczos_matvec", "reorth", "tail", "setup", "spare"]
+        names = ["index", "gram", "lanczos_vec", "lanczos_matvec", "reorth", "tail", "beta_sync", "checks"]
         return dict(zip(names, list(out)))
 
     def reset_timing(self):
