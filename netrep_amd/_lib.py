@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libnetrep_amd.so")
+# NETREP_LIB: another in-tree build of the same library (A/B runs of compile-time variants)
+LIB_PATH = os.environ.get("NETREP_LIB") or os.path.join(_HERE, "_lib", "libnetrep_amd.so")
 
 NR_OK = 0
 NR_ERR_HIP = 1
