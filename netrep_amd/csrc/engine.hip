@@ -252,19 +252,43 @@ int profile_variant_env() {
 }
 
 // Queue order of the summary-profile items. Module-major (every permutation
-// of the largest module, then the next) keeps the largest Grams in flight
-// together: at C3 the 768 slots' first items (modules of 289-300 nodes, a
-// ~350 KB packed Gram plus its Lanczos basis each) overflow the 256 MiB
-// Infinity Cache, so their matvecs stream from HBM. Permutation-major order
-// keeps the size mix of the whole launch in flight; its last T permutations
-// (about one slot's worth of items) run module-major, largest first, so the
-// slots still drain together. NETREP_PROFILE_ORDER_TAIL=0 restores
-// module-major order (A/B runs); any other value fixes T.
-int profile_order_tail(int slots, int n_mod, int64_t n_perm) {
+// of the largest module, then the next: largest-first scheduling) balances
+// the slots best, but keeps the largest Grams in flight together: at C3 the
+// 768 slots' first items (modules of 289-300 nodes, a ~350 KB packed Gram
+// plus its Lanczos basis each, ~365 MB) overflow the 256 MiB Infinity Cache,
+// so their matvecs stream from HBM. Permutation-major order keeps the size
+// mix of the whole launch in flight; its last T permutations (about one
+// slot's worth of items) run module-major, largest first, so the slots still
+// drain together. It is chosen only where it helps: when the largest items'
+// working set would overflow the cache budget and the mix fits it (C3:
+// 18.75 -> 18.17 ms); with Grams that overflow it either way (C5, S = 1000:
+// 445 vs 387 ms module-major) or fit it either way (C2), module-major.
+// NETREP_PROFILE_ORDER_TAIL=0 forces module-major order, any other value
+// permutation-major with that T.
+int profile_order_tail(int slots, const std::vector<int32_t>& k_sorted, int first, int n_mod, int64_t n_perm,
+                       int n_samples, bool dual) {
   if (const char* e = std::getenv("NETREP_PROFILE_ORDER_TAIL")) return std::max(0, std::atoi(e));
   if (n_mod <= 1) return 0;
   const int64_t t = (slots + n_mod - 1) / n_mod;
-  return t >= n_perm ? 0 : (int)t;
+  if (t >= n_perm) return 0;
+  // per-slot working set of a module: packed Gram (+ its fp32 copy) and a
+  // ~40-column Lanczos basis of the Gram's side
+  auto live = [&](int k) {
+    const int side = dual ? std::min(k, n_samples) : k;
+    return (double)nr::packed_gram_doubles(side + 1) * 12.0 + 40.0 * 8.0 * side;
+  };
+  double mix = 0.0;
+  for (int i = 0; i < n_mod; ++i) mix += live(k_sorted[first + i]);
+  mix = mix / n_mod * slots;
+  double top = 0.0;  // the first `slots` items of module-major order
+  int64_t left = slots;
+  for (int i = 0; i < n_mod && left > 0; ++i) {
+    const int64_t c = std::min<int64_t>(left, n_perm);
+    top += live(k_sorted[first + i]) * (double)c;
+    left -= c;
+  }
+  const double budget = 256.0 * (1 << 20);  // the Infinity Cache
+  return (top > budget && mix <= budget) ? (int)t : 0;
 }
 
 // rg4: plan the register-resident 4-wave kernel (variant 5; the caller
@@ -385,7 +409,8 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.scratch = ctx->d_scratch;
     pp.scratch_stride = plan.stride;
     pp.part_global = plan.variant == 4 ? 1 : 0;
-    pp.order_tail = profile_order_tail(plan.slots, seg[i].count, n_perm);
+    pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples,
+                                       plan.dual);
     pp.g32_off = plan.variant == 5 ? 0 : plan.g32_off;
     NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
     if (plan.variant == 5)
