@@ -6,7 +6,10 @@
 // Infinity Cache (N = 20,000: 6.4 GB), for several loads in flight per
 // thread, and the same for 8-byte reads (one of the two matrices alone).
 // Output: reads/s and useful GB/s (the ceiling DESIGN.md quotes for the net
-// kernel's roofline).
+// kernel's roofline). The "cw" lines restrict the column to a window of cw
+// columns (cw x N x 16 bytes: 82 MB at cw = 256, Infinity-Cache resident;
+// 20 MB at 64; 5 MB at 16): the random-read rate a column-block pass of the
+// network kernel would see.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -17,7 +20,7 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 }
 
 template <int U, typename T>
-__global__ void gather(const T* __restrict__ a, int64_t n, int iters, double* out) {
+__global__ void gather(const T* __restrict__ a, int64_t n, int iters, double* out, uint32_t cw) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   double acc = 0.0;
   for (int it = 0; it < iters; ++it) {
@@ -26,7 +29,7 @@ __global__ void gather(const T* __restrict__ a, int64_t n, int iters, double* ou
     for (int u = 0; u < U; ++u) {
       const uint32_t h1 = hash32(tid * 7919u + (uint32_t)(it * U + u) * 104729u);
       const uint32_t h2 = hash32(h1 ^ 0x9E3779B9u);
-      const int64_t r = h1 % (uint32_t)n, c = h2 % (uint32_t)n;
+      const int64_t r = h1 % (uint32_t)n, c = h2 % cw;
       v[u] = a[r + c * n];
     }
 #pragma unroll
@@ -39,21 +42,23 @@ __global__ void gather(const T* __restrict__ a, int64_t n, int iters, double* ou
 }
 
 template <int U, typename T>
-void run(const void* buf, int64_t n, int blocks, int threads, int iters, double* out, const char* name) {
-  hipLaunchKernelGGL((gather<U, T>), dim3(blocks), dim3(threads), 0, 0, (const T*)buf, n, iters, out);
+void run(const void* buf, int64_t n, int blocks, int threads, int iters, double* out, const char* name,
+         uint32_t cw = 0) {
+  if (cw == 0) cw = (uint32_t)n;
+  hipLaunchKernelGGL((gather<U, T>), dim3(blocks), dim3(threads), 0, 0, (const T*)buf, n, iters, out, cw);
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  hipLaunchKernelGGL((gather<U, T>), dim3(blocks), dim3(threads), 0, 0, (const T*)buf, n, iters, out);
+  hipLaunchKernelGGL((gather<U, T>), dim3(blocks), dim3(threads), 0, 0, (const T*)buf, n, iters, out, cw);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
   hipEventElapsedTime(&ms, e0, e1);
   const double reads = (double)blocks * threads * iters * U;
-  printf("%-8s U=%2d blocks=%5d x %4d: %.3f ms  %.2f G reads/s  %.1f GB/s useful\n", name, U, blocks, threads,
-         ms, reads / (ms * 1e-3) / 1e9, reads * sizeof(T) / (ms * 1e-3) / 1e9);
+  printf("%-8s U=%2d blocks=%5d x %4d cw=%6u: %.3f ms  %.2f G reads/s  %.1f GB/s useful\n", name, U, blocks,
+         threads, cw, ms, reads / (ms * 1e-3) / 1e9, reads * sizeof(T) / (ms * 1e-3) / 1e9);
 }
 
 int main() {
@@ -74,5 +79,6 @@ int main() {
   // one 512-thread block per CU, 4 in flight (the fused profile kernel's budget)
   run<4, double2>(buf, n, 256, 512, 64, out, "16B/1wg");
   run<8, double2>(buf, n, 256, 512, 32, out, "16B/1wg");
+  for (uint32_t cw : {1024u, 512u, 256u, 128u, 64u, 16u}) run<8, double2>(buf, n, 2048, 256, 32, out, "16B", cw);
   return 0;
 }
