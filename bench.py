@@ -69,9 +69,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--perms-per-step", type=int, default=0,
-                    help="permutations per step (0: 20 launches of --launch-batch)")
-    ap.add_argument("--launch-batch", "--batch", type=int, default=256, dest="batch",
-                    help="permutations per kernel launch")
+                    help="permutations per step (0: 5,120, at least one launch)")
+    ap.add_argument("--launch-batch", "--batch", type=int, default=1024, dest="batch",
+                    help="permutations per kernel launch (1,024: 51,200 C3 items, short launch tails)")
     ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--no-secondary", action="store_true", help="skip the C4 network-only record")
     ap.add_argument("--secondary-steps", type=int, default=8)
@@ -282,7 +282,7 @@ def main():
     world, rank, local = setup_dist(args)
     eng, lay, meta, tensors = build_case(args.config, world, rank, local, args.seed)
     B, K, W = args.batch, args.steps, args.warmup
-    P = args.perms_per_step or 20 * B
+    P = args.perms_per_step or max(5120, B)
     eng.set_batch(B)
     net_b, prof_b, prof_f = roofline_terms(lay.module_sizes, meta["n_samples"], meta["with_data"])
     n_cfg, s_cfg, sizes_cfg, _, _ = S.CONFIGS[args.config]
