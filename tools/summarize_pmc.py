@@ -1,4 +1,5 @@
-"""Summarise tools/collect_pmc.sh output per engine kernel (mean per dispatch).
+"""Summarise tools/collect_pmc.sh output per engine kernel (mean per full-size
+dispatch: the bench's timed launches, without its one-permutation launches).
 
 FETCH_SIZE/WRITE_SIZE are in KB. Following MI355X_MICROARCH.md (HBM section),
 FETCH_SIZE reads 1/2 of the bytes of wide coalesced streams on gfx950; the
@@ -27,21 +28,36 @@ def load(path):
     return agg
 
 
+def full_size(values):
+    """Indices of the full-size dispatches: the bench's timed launches, not the
+    one-permutation launches of the observed statistics and discovery vectors
+    (>= 10% of the largest dispatch's count)."""
+    top = max(values) if values else 0.0
+    return [i for i, v in enumerate(values) if v >= 0.1 * top]
+
+
 def main():
     out = sys.argv[1]
     res = defaultdict(dict)
     for sub in ("fetch", "write", "tcc", "sq", "mfma"):
         for k, cs in load(os.path.join(out, sub, "run_counter_collection.csv")).items():
+            first = next(iter(cs.values()))
+            keep = full_size(first)  # the pass's first counter sizes its dispatches
             for c, v in cs.items():
-                res[k][c] = sum(v) / len(v)
-                res[k]["dispatches_" + sub] = len(v)
-    stats = os.path.join(out, "trace", "run_kernel_stats.csv")
-    if os.path.exists(stats):
-        for r in csv.DictReader(open(stats)):
-            if "nr::" in r["Name"]:
-                key = r["Name"].split("(")[0].replace("void ", "")
-                res[key]["avg_ns"] = float(r["AverageNs"])
-                res[key]["calls"] = int(r["Calls"])
+                kept = [v[i] for i in keep if i < len(v)]
+                res[k][c] = sum(kept) / len(kept)
+                res[k]["dispatches_" + sub] = len(kept)
+    trace = os.path.join(out, "trace", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        dur = defaultdict(list)
+        for r in csv.DictReader(open(trace)):
+            if "nr::" in r["Kernel_Name"]:
+                key = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                dur[key].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+        for key, v in dur.items():
+            kept = [v[i] for i in full_size(v)]
+            res[key]["avg_ns"] = sum(kept) / len(kept)
+            res[key]["calls"] = len(kept)
     for k, d in res.items():
         if "FETCH_SIZE" in d:
             d["hbm_bytes_corrected"] = d["FETCH_SIZE"] * 1024 * 2 + d.get("WRITE_SIZE", 0.0) * 1024
