@@ -592,7 +592,20 @@ int64_t auto_batch(const nr_ctx* ctx) {
   // permutations (51,200 items) per launch runs 3.5% faster than at 256
   // (profiles/r02/profile_variants.txt). Per-slot scratch does not depend on it.
   const int64_t items_target = ctx->d_data ? 51200 : 65536;
-  return std::max<int64_t>(1, items_target / std::max<int32_t>(ctx->n_present, 1));
+  int64_t b = std::max<int64_t>(1, items_target / std::max<int32_t>(ctx->n_present, 1));
+  if (ctx->d_data) {
+    // ... but launches of heavy modules stay short (~0.1 s), so progress and
+    // interrupts keep their one-second cadence (src/thread-utils.cpp:49-82):
+    // at most 2e12 Gram flops (2 S k min(S, k) per module) per launch; C3 at
+    // 1,024 permutations is 1.7e12, C5 (k up to 2,000, S = 1,000) gets 66.
+    double per_perm = 0.0;
+    for (const int32_t k : ctx->order_k_h) {
+      const double kk = (double)k, s = (double)ctx->n_samples;
+      per_perm += 2.0 * s * kk * std::min(s, kk);
+    }
+    if (per_perm > 0.0) b = std::min<int64_t>(b, std::max<int64_t>(1, (int64_t)(2e12 / per_perm)));
+  }
+  return b;
 }
 
 int check_ready(nr_ctx* ctx, bool need_null) {
