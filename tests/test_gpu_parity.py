@@ -233,6 +233,33 @@ def test_batching_and_sharding_are_bitwise_invariant():
     assert d == t == 7
 
 
+def test_queue_order_is_bitwise_invariant(monkeypatch):
+    """Every item is computed by one workgroup on its own: module-major and
+    permutation-major queue orders (engine.hip profile_order_tail) give the
+    same cube bit for bit."""
+    lay, mi, disc, tx, tc, tn = _engine_case()
+    eng = _engine_from(mi, disc, tx, tc, tn)
+    monkeypatch.setenv("NETREP_PROFILE_ORDER_TAIL", "0")
+    a = eng.run(0, 24, 5)
+    monkeypatch.setenv("NETREP_PROFILE_ORDER_TAIL", "3")
+    b = eng.run(0, 24, 5)
+    np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+@pytest.mark.parametrize("relax", ["0", "1"])
+def test_relaxed_lanczos_steps_vs_oracle(relax, monkeypatch):
+    """fp32 matvecs after the residual drops below 1e-7 theta (kernels.hip
+    lanczos_ritz) keep the parity bar, primal (k <= S) and dual (k > S) Grams."""
+    monkeypatch.setenv("NETREP_RELAX", relax)
+    lay, mi, disc, tx, tc, tn = _engine_case(n_samples=60, sizes=(30, 45, 60, 80, 120))
+    eng = _engine_from(mi, disc, tx, tc, tn)
+    seed = 77
+    nulls = eng.run(0, 8, seed)
+    pis = np.stack([prp.permute(np.arange(mi.null_idx.size), mi.null_idx.size, seed, p) for p in range(8)])
+    exp, _ = O.permutation_procedure(disc, tx, tc, tn, mi, pis.astype(np.int64))
+    assert_stats_close(nulls, exp, what=f"nulls (NETREP_RELAX={relax})")
+
+
 def test_constant_column_gives_na():
     """A node with constant data scales to NaN; summary-profile stats of any module
     containing it become NA (svd_econ failure path, src/netStats.cpp:229-235)."""
