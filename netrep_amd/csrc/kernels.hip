@@ -987,8 +987,8 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     s_reorth = 0;
     flags[5] = 0;  // relaxed (fp32) matvecs
   }
+  for (int c = tid; c < k; c += BS) Q[c] = q[c];  // q_0 (later q_j are stored by the update below)
   for (int j = 0; j < mcap; ++j) {
-    for (int c = tid; c < k; c += BS) Q[(int64_t)j * k + c] = q[c];
     NR_STAMP(2);  // Lanczos: vector updates / tridiagonal checks
     // Barriers per step: the matvec's combine and its sum, the 3-term norm,
     // the omega decision, and one after the q update (+ one per check). The
@@ -1029,11 +1029,14 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       beta[j] = beta_j;
     }
     nsteps = j + 1;
-    {  // next Lanczos vector (unused if this step's check ends the run)
+    {  // next Lanczos vector (unused if this step's check ends the run), into the basis too
       const double inv = 1.0 / beta_j;
+      double* qn = j + 1 < mcap ? Q + (int64_t)(j + 1) * k : nullptr;
       for (int c = tid; c < k; c += BS) {
         qprev[c] = q[c];
-        q[c] = w[c] * inv;
+        const double v = w[c] * inv;
+        q[c] = v;
+        if (qn) qn[c] = v;
       }
     }
     beta_prev = beta_j;
