@@ -243,6 +243,13 @@ bool relax_enabled() {
   return !(f && f[0] == '0');
 }
 
+// Lanczos start vector: the Gram column of largest norm (kernels.hip
+// start_column); on unless NETREP_START_COL=0 (A/B runs).
+bool start_col_enabled() {
+  const char* f = std::getenv("NETREP_START_COL");
+  return !(f && f[0] == '0');
+}
+
 // NETREP_PROFILE_VARIANT (A/B runs): -1 when unset.
 int profile_variant_env() {
   const char* f = std::getenv("NETREP_PROFILE_VARIANT");
@@ -412,6 +419,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples,
                                        plan.dual);
     pp.g32_off = plan.variant == 5 ? 0 : plan.g32_off;
+    pp.start_col = start_col_enabled() ? 1 : 0;
     NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
     if (plan.variant == 5)
       NR_HIP(ctx, nr::launch_profile_rg4(pp, plan.slots, st));

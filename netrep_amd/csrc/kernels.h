@@ -83,6 +83,8 @@ struct ProfileParams {
   int64_t basis_doubles;       // Lanczos basis doubles per slot (behind the Gram)
   int64_t g32_off;             // doubles from the slot start to the fp32 copy of the packed Gram
                                // (relaxed Lanczos steps; 0: no copy, fp64 matvecs throughout)
+  int32_t start_col;           // 1: Lanczos starts from the packed Gram's column of largest norm
+                               // (its node's row of G), 0: from the near-constant vector
   int32_t order_tail;          // queue order: 0 = module-major (large modules first); T > 0 =
                                // permutation-major over all modules (a size mix in flight) for the
                                // first n_perm - T permutations, the last T module-major
