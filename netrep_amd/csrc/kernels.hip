@@ -20,6 +20,14 @@
 #include "kernels.h"
 #include "device_common.h"
 
+// Gram operand pipeline depth (register buffers per wave: 2 = one 16-row step
+// in flight, 3 = two); compile-time A/B via -DNR_GRAM_DEPTH=3. Depth 3 spills
+// in the 3-workgroup kernel (scratch 184 -> 260 B/lane) and measured slower on
+// C3: 72.3 vs 68.8 ms per 1,024-permutation launch (profiles/r02/profile_variants.txt).
+#ifndef NR_GRAM_DEPTH
+#define NR_GRAM_DEPTH 2
+#endif
+
 namespace nr {
 
 
@@ -623,7 +631,28 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
         acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[1][q], v[3][q], acc[1][1], 0, 0, 0);
       }
     };
-    double cur[4][4], nxt[4][4];
+    double cur[4][4];
+#if NR_GRAM_DEPTH >= 3
+    // two steps in flight: three register buffers in rotation; the loads are
+    // unconditional (clamped to the last full step, the surplus unused) so
+    // every wait is a static vmcnt that leaves the later buffers in flight
+    double b1[4][4], b2[4][4];
+    if (full > 0) {
+      ld16(0, cur);
+      ld16(min(16, full - 16), b1);
+    }
+    for (int s0 = 0; s0 < full; s0 += 48) {
+      ld16(min(s0 + 32, full - 16), b2);
+      mfma16(cur);
+      if (s0 + 16 >= full) break;
+      ld16(min(s0 + 48, full - 16), cur);
+      mfma16(b1);
+      if (s0 + 32 >= full) break;
+      ld16(min(s0 + 64, full - 16), b1);
+      mfma16(b2);
+    }
+#else
+    double nxt[4][4];
     if (full > 0) ld16(0, cur);
     for (int s0 = 0; s0 < full; s0 += 16) {
       if (s0 + 16 < full) ld16(s0 + 16, nxt);
@@ -633,6 +662,7 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
 #pragma unroll
         for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
     }
+#endif
     if (full < S) {  // the last, partial step
 #pragma unroll
       for (int o = 0; o < 4; ++o)
