@@ -13,6 +13,7 @@
 // (src/properties.cpp:155-184).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 #include <math.h>
 
@@ -814,54 +815,78 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
   double up[16];
 #pragma unroll
   for (int t = 0; t < 16; ++t) up[t] = 0.0;
-  for (int u = u0; u < u1; ++u) {
-    const int c0 = cg * 16;
-    const int L = P - c0;
-    const int h = min(64, L - 64 * j);
-    const int r = c0 + 64 * j + lane;
-    const double xr = SQ ? (r < k ? 1.0 : 0.0) : (r < k ? x[r] : 0.0);  // SQ: row mask
-    const int vo = lane < h ? lane * EB : (int)0x80000000;
-    int so = (int)(pk_base(cg, P) + 1024 * j) * EB;
-    double g[16];
+  // Units in flight per wave: the fp32 pieces of two units occupy the
+  // registers of one fp64 unit, so the relaxed (F32) passes issue two units'
+  // loads (32 per lane) before the first wait; the matvec is latency-bound at
+  // three workgroups per CU, not byte-bound (profiles/r02/profile_variants.txt).
+  // A unit beyond the wave's range loads nothing (range-checked offsets).
+  constexpr int UF = F32 ? 2 : 1;
+  using LT = typename std::conditional<F32, float, double>::type;
+  for (int u = u0; u < u1; u += UF) {
+    LT gb[UF][16];
+    {
+      int lcg = cg, lj = j;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      if (F32)
-        g[t] = (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo, so, 0));
-      else
-        g[t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
-      so += h * EB;
-    }
-    double acc = 0.0;
-    if (SQ) {
+      for (int i = 0; i < UF; ++i) {
+        const bool valid = u + i < u1;
+        const int h = min(64, P - 16 * lcg - 64 * lj);
+        const int vo = valid && lane < h ? lane * EB : (int)0x80000000;
+        int so = valid ? (int)(pk_base(lcg, P) + 1024 * lj) * EB : 0;
 #pragma unroll
-      for (int t = 0; t < 16; ++t) acc += c0 + t < k ? g[t] * g[t] : 0.0;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) g[t] *= g[t];  // the mirrored part below sums squares too
-    } else {
-      const double xl = c0 + (lane & 15) < k ? x[c0 + (lane & 15)] : 0.0;  // the unit's 16 x_c, one per lane
-#pragma unroll
-      for (int t = 0; t < 16; ++t) acc += g[t] * nr_readlane_f64(xl, t);  // (saves 30 VGPRs over 16 LDS reads)
-    }
-    if (j > 0) {
-#pragma unroll
-      for (int t = 0; t < 16; ++t) up[t] += g[t] * xr;
-    } else {  // the chunk holding the group's diagonal block
-#pragma unroll
-      for (int t = 0; t < 16; ++t) up[t] += (r > c0 + t) ? g[t] * xr : 0.0;
-    }
-    if (r < k) part[wave * ks + r] += acc;
-    ++j;
-    if (j == nj || u + 1 == u1) {
-      const double v = nr_transpose_reduce16(up, lane);
-      if ((lane & 3) == 0) {
-        const int c = c0 + ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
-        if (c < k) part[wave * ks + c] += v;
+        for (int t = 0; t < 16; ++t) {
+          if (F32)
+            gb[i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo, so, 0));
+          else
+            gb[i][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
+          so += h * EB;
+        }
+        if (++lj == ((P - 16 * lcg + 63) >> 6)) {
+          ++lcg;
+          lj = 0;
+        }
       }
+    }
 #pragma unroll
-      for (int t = 0; t < 16; ++t) up[t] = 0.0;
-      ++cg;
-      j = 0;
-      nj = (P - 16 * cg + 63) >> 6;
+    for (int i = 0; i < UF; ++i) {
+      if (u + i >= u1) break;
+      const int c0 = cg * 16;
+      const int r = c0 + 64 * j + lane;
+      const double xr = SQ ? (r < k ? 1.0 : 0.0) : (r < k ? x[r] : 0.0);  // SQ: row mask
+      // one pass over the unit's 16 pieces, each converted where it is used
+      // (no 16-double copy next to the next unit's pieces in flight)
+      const bool diag = j == 0;  // the chunk holding the group's diagonal block
+      double acc = 0.0;
+      if (SQ) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const double gt = (double)gb[i][t];
+          const double g2 = gt * gt;  // the mirrored part sums squares too
+          acc += c0 + t < k ? g2 : 0.0;
+          up[t] += (!diag || r > c0 + t) ? g2 * xr : 0.0;
+        }
+      } else {
+        const double xl = c0 + (lane & 15) < k ? x[c0 + (lane & 15)] : 0.0;  // the unit's 16 x_c, one per lane
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const double gt = (double)gb[i][t];
+          acc += gt * nr_readlane_f64(xl, t);  // (saves 30 VGPRs over 16 LDS reads)
+          up[t] += (!diag || r > c0 + t) ? gt * xr : 0.0;
+        }
+      }
+      if (r < k) part[wave * ks + r] += acc;
+      ++j;
+      if (j == nj || u + i + 1 == u1) {
+        const double v = nr_transpose_reduce16(up, lane);
+        if ((lane & 3) == 0) {
+          const int c = c0 + ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+          if (c < k) part[wave * ks + c] += v;
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) up[t] = 0.0;
+        ++cg;
+        j = 0;
+        nj = (P - 16 * cg + 63) >> 6;
+      }
     }
   }
   __syncthreads();
