@@ -470,14 +470,14 @@ __device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mm
 template <int NW, class MV, class DG>
 __device__ __forceinline__ void profile_contrib(const ProfileParams& P, int k, int m, const LzLds& L,
                                                 const double* __restrict__ X, int S, double ones_g_ones,
-                                                MV& mv, DG diag) {
+                                                MV& mv, DG diag, bool gv_ready = false) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x;
   const double Sd = (double)S;
   double* vv = L.vv;
   double* gv = L.gv;
   double* colm = L.colm;
-  mv(vv, gv, nullptr);
+  if (!gv_ready) mv(vv, gv, nullptr);  // else lanczos_ritz left G v in L.gv
   // lambda = v.Gv; ubar = mean of u = X v / sigma
   double a3[2] = {0.0, 0.0};
   for (int c = tid; c < k; c += BS) {

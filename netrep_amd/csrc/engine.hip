@@ -250,6 +250,13 @@ bool start_col_enabled() {
   return !(f && f[0] == '0');
 }
 
+// G v of the Ritz vector from the Lanczos relation (kernels.hip lanczos_ritz);
+// on unless NETREP_GV_RELATION=0 (A/B runs).
+bool gv_relation_enabled() {
+  const char* f = std::getenv("NETREP_GV_RELATION");
+  return !(f && f[0] == '0');
+}
+
 // NETREP_PROFILE_VARIANT (A/B runs): -1 when unset.
 int profile_variant_env() {
   const char* f = std::getenv("NETREP_PROFILE_VARIANT");
@@ -420,6 +427,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
                                        plan.dual);
     pp.g32_off = plan.variant == 5 ? 0 : plan.g32_off;
     pp.start_col = start_col_enabled() ? 1 : 0;
+    pp.gv_relation = gv_relation_enabled() ? 1 : 0;
     NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
     if (plan.variant == 5)
       NR_HIP(ctx, nr::launch_profile_rg4(pp, plan.slots, st));

@@ -85,6 +85,8 @@ struct ProfileParams {
                                // (relaxed Lanczos steps; 0: no copy, fp64 matvecs throughout)
   int32_t start_col;           // 1: Lanczos starts from the packed Gram's column of largest norm
                                // (its node's row of G), 0: from the near-constant vector
+  int32_t gv_relation;         // 1: G v of the Ritz vector from the Lanczos relation (no extra
+                               // fp64 matvec; primal Gram only), 0: one more matvec
   int32_t order_tail;          // queue order: 0 = module-major (large modules first); T > 0 =
                                // permutation-major over all modules (a size mix in flight) for the
                                // first n_perm - T permutations, the last T module-major

@@ -1062,7 +1062,7 @@ __device__ __forceinline__ double reorthogonalise_bf(const double* __restrict__ 
 template <int NW, bool BF, class MV>
 __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, const LzLds& L, int* flags,
                                              double* Q, MV& mv, uint64_t& t_mark, bool* relax = nullptr,
-                                             bool q_given = false) {
+                                             bool q_given = false, bool gv_out = false) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mmax = L.mmax;
@@ -1182,7 +1182,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
           s_done = conv || last || !(beta_j > 1e-300 * fabs(theta));
           if (relax && resid <= 1e-7 * fabs(theta)) flags[5] = 1;
           // the Ritz vector's coefficients: inverse iteration (LU), once
-          if (s_done) tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
+          if (s_done) {
+            tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
+            L.h[0] = theta;  // for gv_out (h is idle once the run ends)
+          }
           if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
           int step = 8;
           if (prev_j > 0 && resid < prev_r && resid > 0.0) {
@@ -1207,12 +1210,21 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     atomicAdd(P.diag + 1, 1);
     atomicAdd(P.diag + 2, nsteps);
   }
-  // Ritz vector v = Q y, normalised
+  // Ritz vector v = Q y, normalised. gv_out: also G v into L.gv from the
+  // Lanczos relation G Q y = Q T y + w y_m = theta Q y + y_m w (w = beta_m
+  // q_{m+1}, still in L.w), instead of one more fp64 pass over G. Rounding,
+  // the relaxed fp32 steps and the projections a reorthogonalisation drops
+  // perturb it by sum_j |y_j| |E_j|: the same terms the relaxed Krylov
+  // argument already bounds for the Ritz vector, on coefficients y_j that are
+  // at the residual's level once those steps start.
   double nv[1] = {0.0};
+  const double theta_f = gv_out ? L.h[0] : 0.0;
+  const double ym = gv_out ? ty[nsteps - 1] : 0.0;
   for (int c = tid; c < k; c += BS) {
     double s = 0.0;
     for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
     L.vv[c] = s;
+    if (gv_out) L.gv[c] = theta_f * s + ym * w[c];
     nv[0] += s * s;
   }
   if (BF)  // twork (the packed matvec's partials) held the tridiagonal LU: zero again
@@ -1220,7 +1232,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   block_sums<1, NW>(nv, red);
   {
     const double inv = 1.0 / sqrt(nv[0]);
-    for (int c = tid; c < k; c += BS) L.vv[c] *= inv;
+    for (int c = tid; c < k; c += BS) {
+      L.vv[c] *= inv;
+      if (gv_out) L.gv[c] *= inv;
+    }
   }
   __syncthreads();
 }
@@ -1319,14 +1334,15 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
                      : packed_matvec<NW>(G, kc, n, x, out, part, kmax, y, L.red);
       };
       const bool q_given = PACKED && P.start_col && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
-      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given);
+      const bool gv_rel = P.gv_relation && !dual;
+      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel);
       relax = false;  // node contributions: the fp64 Gram
       if (dual) {
         profile_contrib_dual<NW>(P, k, m, Li, X, S, g1[0]);
       } else {
         profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) {
           return PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
-        });
+        }, gv_rel);
       }
     } else {
       profile_nonfinite<NW>(P, k, m, S, Li);
