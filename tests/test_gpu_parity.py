@@ -260,6 +260,24 @@ def test_relaxed_lanczos_steps_vs_oracle(relax, monkeypatch):
     assert_stats_close(nulls, exp, what=f"nulls (NETREP_RELAX={relax})")
 
 
+@pytest.mark.parametrize("start_col,gv_rel", [("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")])
+def test_lanczos_start_and_gv_relation_vs_oracle(start_col, gv_rel, monkeypatch):
+    """The Lanczos start G e_c* (kernels.hip start_column) and the Ritz
+    vector's G v from the Lanczos relation, each on and off: same parity bar,
+    primal (k <= S) and dual (k > S) Grams, and bitwise reproducible."""
+    monkeypatch.setenv("NETREP_START_COL", start_col)
+    monkeypatch.setenv("NETREP_GV_RELATION", gv_rel)
+    lay, mi, disc, tx, tc, tn = _engine_case(n_samples=60, sizes=(30, 45, 60, 80, 120))
+    eng = _engine_from(mi, disc, tx, tc, tn)
+    seed = 91
+    nulls = eng.run(0, 8, seed)
+    pis = np.stack([prp.permute(np.arange(mi.null_idx.size), mi.null_idx.size, seed, p) for p in range(8)])
+    exp, _ = O.permutation_procedure(disc, tx, tc, tn, mi, pis.astype(np.int64))
+    assert_stats_close(nulls, exp, what=f"nulls (NETREP_START_COL={start_col}, NETREP_GV_RELATION={gv_rel})")
+    again = eng.run(0, 8, seed)
+    assert np.array_equal(nulls.view(np.uint64), again.view(np.uint64))
+
+
 def test_constant_column_gives_na():
     """A node with constant data scales to NaN; summary-profile stats of any module
     containing it become NA (svd_econ failure path, src/netStats.cpp:229-235)."""
