@@ -1059,6 +1059,9 @@ __device__ __forceinline__ double reorthogonalise_bf(const double* __restrict__ 
 // accuracy: the later a step, the smaller its weight in the Ritz vector;
 // offline study on C3 null items, tools/sim_lanczos_relax.py: same steps, same
 // 2e-14 worst eigenvector error as fp64 throughout, 19% fewer Gram bytes).
+// q_given: start from the vector the caller left in L.q (start_column's
+// G e_c*) instead of the near-constant one. gv_out: also leave G v in L.gv,
+// from the Lanczos relation (see the end of the function).
 template <int NW, bool BF, class MV>
 __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, const LzLds& L, int* flags,
                                              double* Q, MV& mv, uint64_t& t_mark, bool* relax = nullptr,
