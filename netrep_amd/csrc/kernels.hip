@@ -595,7 +595,10 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
   const int T2 = (kc + 31) / 32;
   const int nsup = T2 * (T2 + 1) / 2;
   const int full = S / 16 * 16;  // steps whose 16 rows are all in range
-  for (int t = wave; t < nsup; t += NW) {
+  // Whole rounds of super-tiles (one per wave); the last nsup % NW are cut into
+  // their 16 x 16 tiles below, dealt over every wave (load balance).
+  const int nfull = nsup - nsup % NW;
+  for (int t = wave; t < nfull; t += NW) {
     int I2 = 0, rem = t;
     while (rem >= T2 - I2) { rem -= T2 - I2; ++I2; }
     const int J2 = I2 + rem;
@@ -691,6 +694,69 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
           if (gi == gj && gi < k) bad |= (int)!isfinite(val);
         }
       }
+  }
+  // The remainder round: 4 (nsup % NW) single tiles over the NW waves, each
+  // with one accumulator fed by its two 16-column operand blocks (same K
+  // order as the super-tile path, so every G entry is bitwise the same).
+  const int nsub = 4 * (nsup - nfull);
+  for (int u = wave; u < nsub; u += NW) {
+    const int t = nfull + (u >> 2), a = (u >> 1) & 1, b = u & 1;
+    int I2 = 0, rem = t;
+    while (rem >= T2 - I2) { rem -= T2 - I2; ++I2; }
+    const int J2 = I2 + rem;
+    const double* cp[2];
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int c = (o == 0 ? I2 * 32 + 16 * a : J2 * 32 + 16 * b) + i16;
+      const int64_t off = c < k ? (int64_t)idx[c] * S : (c == k ? ones_off : ones_off + S);
+      cp[o] = X + off + 4 * kk;
+    }
+    nr_f64x4 acc1 = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+    auto ld4 = [&](int s0, double (&v)[2][4]) {
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+        double2 p0, p1;
+        __builtin_memcpy(&p0, cp[o] + s0, sizeof(double2));
+        __builtin_memcpy(&p1, cp[o] + s0 + 2, sizeof(double2));
+        v[o][0] = p0.x;
+        v[o][1] = p0.y;
+        v[o][2] = p1.x;
+        v[o][3] = p1.y;
+      }
+    };
+    double c1[2][4], n1[2][4];
+    if (full > 0) ld4(0, c1);
+    for (int s0 = 0; s0 < full; s0 += 16) {
+      if (s0 + 16 < full) ld4(s0 + 16, n1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(c1[0][q], c1[1][q], acc1, 0, 0, 0);
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c1[o][q] = n1[o][q];
+    }
+    if (full < S) {  // the last, partial step
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c1[o][q] = full + 4 * kk + q < S ? cp[o][full + q] : 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(c1[0][q], c1[1][q], acc1, 0, 0, 0);
+    }
+    const double wgt = (I2 == J2) ? 1.0 : 2.0;
+    if (PACKED) pk_store_tile(G, G32, kc, I2, J2, a, b, acc1, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = I2 * 32 + 16 * a + kk + 4 * r;
+      const int gj = J2 * 32 + 16 * b + i16;
+      const double val = acc1[r];
+      if (!PACKED) {
+        G[gi + (int64_t)gj * ld] = val;
+        G[gj + (int64_t)gi * ld] = val;
+      }
+      if (gi < k && gj < k) g1sum += wgt * val;
+      if (gi == gj && gi < k) bad |= (int)!isfinite(val);
+    }
   }
 }
 
