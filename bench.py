@@ -63,6 +63,25 @@ def measured_traffic(config, batch, kernel):
     return None
 
 
+def measured_mfma(config, batch, kernel, avg_ms):
+    """Executed fp64 MFMA work of `kernel` from the same committed PMC pass
+    (SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 flops per launch, tools/summarize_pmc.py),
+    as TFLOP/s over this run's HIP-event launch time, and the MFMA-busy share
+    (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1,024 SIMDs); None
+    when no pass matches."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for r in rows:
+        if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
+                and "mfma_f64_flops_executed" in r and avg_ms > 0):
+            return {"executed_TFLOPs": round(r["mfma_f64_flops_executed"] / (avg_ms * 1e-3) / 1e12, 4),
+                    "mfma_busy_pct": round(r.get("mfma_busy_pct", float("nan")), 2)}
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -369,6 +388,8 @@ def main():
                                     "+ WRITE_SIZE, profiles/pmc_traffic.json)",
                     "algorithmic_bytes": round(((net_b if fused or dom_name == "module_net_kernel" else 0.0)
                                                 + (prof_b if dom_name == "module_profile_kernel" else 0.0)) * B)}
+        if dom["unit"] == "TFLOP/s":  # executed MFMA flops next to the algorithmic figure (PMC pass)
+            roofline["executed"] = measured_mfma(args.config, B, dom_name, dom.get("avg_ms", 0.0))
         cpu = None
         if world == 1 and not args.no_cpu_baseline and host is not None:
             rate, dt, n_cpu, threads = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)
