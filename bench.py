@@ -100,6 +100,9 @@ def parse():
                     help="CPU sample size (0: sized for ~15 s on the host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--c5-single", action="store_true",
+                    help="C5 as one device-resident test dataset on the engine layer (round 2's C5 record) "
+                         "instead of three host datasets through the reference interface")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic run: per-phase cycle stamps in the profile kernel")
     return ap.parse_args()
@@ -128,15 +131,20 @@ def relaunch_if_needed(args):
 
 
 def setup_dist(args):
+    """One process per GPU. The backend is RCCL ("nccl") -- broadcasts over
+    xGMI; NETREP_BENCH_BACKEND=gloo runs the same path over gloo (the -m gpu
+    test of the sharded HIP path puts two ranks on one GPU that way)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        backend = os.environ.get("NETREP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -270,13 +278,37 @@ def time_steps(eng, world, rank, steps, warmup, perms_per_step, seed, base_warm)
     return elapsed, chunks, total
 
 
+def host_cores():
+    """The host CPU as this process sees it: the machine's logical CPUs
+    (nproc), the ones this process may run on (affinity), the CPU model, and
+    the GPU lease's share of them (OMP_NUM_THREADS, 16 per GPU on the box)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, affinity)
+    return {"nproc": os.cpu_count() or 1, "affinity": affinity, "lease_share": share, "model": model}
+
+
 def cpu_baseline(lay, meta, host, n_perm, seed):
     """The C++ CPU restatement of the reference's path (oracle/netrep_ref.cpp:
-    per-thread contiguous permutation chunks, one null-pool shuffle per
-    permutation, LAPACK dgesvd per module) on a bounded sample of the same
-    workload, using the host cores of this GPU's share (at most 16)."""
+    per-thread contiguous permutation chunks as src/permutations.cpp:338-373,
+    one null-pool shuffle per permutation, LAPACK dgesvd per module) on a
+    bounded sample of the same workload, on every host core of this GPU's
+    lease (the box gives a one-GPU command its share of the machine:
+    OMP_NUM_THREADS; nproc shows the whole machine)."""
     from oracle import ref_cpp
-    threads = max(1, min(16, os.cpu_count() or 1))
+    hc = host_cores()
+    threads = max(1, min(hc["lease_share"], hc["affinity"]))
     tc = host["tc"].cpu().numpy()
     tn = host["tn"].cpu().numpy()
     tx = host["txs"].cpu().numpy().T if meta["with_data"] else None   # S x N view, column-major
@@ -294,13 +326,156 @@ def cpu_baseline(lay, meta, host, n_perm, seed):
     t0 = time.perf_counter()
     ref_cpp.permutation_procedure(tx, tc, tn, n_perm=n_perm, **args)
     dt = time.perf_counter() - t0
-    return n_perm / dt, dt, n_perm, threads
+    return n_perm / dt, dt, n_perm, threads, hc
+
+
+def run_c5(args, world, rank, local):
+    """BASELINE.json configs[4] as stated: 40,000 genes x 1,000 samples,
+    modules of geomspace(30, 2000, 40) genes, THREE test datasets,
+    null = "all" -- through the reference interface, as modulePreservation
+    drives it (one PermutationProcedure per test dataset,
+    R/modulePreservation.R:553-635). The discovery modules cover 30,000 of
+    the genes; each test dataset holds all 40,000 in its own column order, so
+    the "all" pool (the test colnames, src/permutations.cpp:317-323) is larger
+    than the module nodes. The test matrices start in host memory (as R holds
+    them): dataset t+1 is uploaded by netrep_PrefetchTestDataset while
+    dataset t's permutations run. A step = --perms-per-step permutations of
+    each of the three datasets; value = permutations / wall time of the
+    pipelined loop. Upload alone and compute alone are timed separately."""
+    if world != 1:
+        raise SystemExit("--config C5 (three test datasets through the reference interface) is a one-GPU run")
+    from netrep_amd.api import RMatrix
+    n, s, sizes, _, _ = S.CONFIGS["C5"]
+    seed = args.seed
+    n_disc = 30_000
+    rng = np.random.default_rng(seed)
+    all_names = [f"G{i}" for i in range(n)]
+    disc_pos = np.sort(rng.choice(n, n_disc, replace=False))
+    lay_d = S.make_layout(n_disc, sizes, seed)
+    d_names = [all_names[i] for i in disc_pos]
+    ma = dict(zip(d_names, lay_d.labels))
+    modules = lay_d.modules
+    dev = torch.device("cuda", local)
+    t_setup = time.perf_counter()
+    dx, dc, dn = S.torch_dataset(lay_d, s, seed + 1, device=dev)
+    dxs = scale_rows(dx).contiguous()
+    del dx
+    torch.cuda.synchronize()
+    eng = N.Engine(local)
+    eng.set_dataset_device(dc.data_ptr(), dn.data_ptr(), dxs.data_ptr(), n_disc, s)
+    node_off, idx = S.csr_of(lay_d)
+    v = eng.module_vectors(node_off, idx, True)
+    eng.close()
+    del dxs, dc, dn
+    torch.cuda.empty_cache()
+    disc = {"degree": {}, "corr": {}, "contribution": {}}
+    o = ocv = 0
+    for m in modules:
+        k = lay_d.members[m].size
+        disc["degree"][m] = v["degree"][o:o + k]
+        disc["contribution"][m] = v["contribution"][o:o + k]
+        disc["corr"][m] = v["corr"][ocv:ocv + k * (k - 1) // 2]
+        o += k
+        ocv += k * (k - 1) // 2
+    datasets = []
+    for t in range(3):
+        order = np.random.default_rng(seed + 10 + t).permutation(n)
+        t_names = [all_names[i] for i in order]
+        pos_of = {nm: j for j, nm in enumerate(t_names)}
+        lay_t = S.Layout(n, sizes, t_names, ["0"] * n, modules,
+                         {m: np.sort(np.array([pos_of[d_names[i]] for i in lay_d.members[m]])) for m in modules})
+        tx, tc, tn = S.torch_dataset(lay_t, s, seed + 20 + t, preserve_all=(t == 0), device=dev)
+        txs = scale_rows(tx)
+        del tx
+        # host copies, column-major (the matrices are symmetric: the transposed
+        # view of the row-major copy is the column-major matrix)
+        tcn, tnn = tc.cpu().numpy().T, tn.cpu().numpy().T
+        txn = np.asfortranarray(txs.cpu().numpy().T)
+        del tc, tn, txs
+        torch.cuda.empty_cache()
+        datasets.append((RMatrix(txn, None, t_names), RMatrix(tcn, t_names, t_names), RMatrix(tnn, t_names, t_names)))
+    t_setup = time.perf_counter() - t_setup
+    P = args.perms_per_step or 256
+    K, W = args.steps, args.warmup
+
+    def one_pass(step):
+        N.PrefetchTestDataset(*datasets[0])
+        for t in range(3):
+            if t + 1 < 3:
+                N.PrefetchTestDataset(*datasets[t + 1])   # uploads while dataset t runs
+            r = N.PermutationProcedure(disc, *datasets[t], ma, modules, P, nullHypothesis="all",
+                                       seed=seed + 1000 * step + t)
+        return r
+
+    for w in range(W):
+        one_pass(-1 - w)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k_ in range(K):
+        last = one_pass(k_)
+    elapsed = time.perf_counter() - t0
+    finite = float(np.isfinite(last["nulls"]).mean())
+    # upload alone (pinned double-buffered chunks, 25.9 GB per dataset) and
+    # compute alone (dataset resident) on one dataset, engine layer
+    x, c, nt = datasets[0]
+    e2 = N.Engine(local)
+    t1 = time.perf_counter()
+    e2.set_dataset(c.f, nt.f, x.f)
+    upload_s = time.perf_counter() - t1
+    names0 = list(nt.colnames)
+    pos0 = {nm: j for j, nm in enumerate(names0)}
+    idx_t = np.concatenate([[pos0[d_names[i]] for i in lay_d.members[m]] for m in modules]).astype(np.int32)
+    e2.set_modules(len(modules), np.arange(len(modules)), node_off, idx_t, idx_t, v["corr"], v["degree"],
+                   v["contribution"])
+    e2.set_null_pool(np.arange(n, dtype=np.int32))
+    e2.run(0, 8, seed)
+    e2.synchronize()
+    e2.set_timing(True)
+    e2.reset_timing()
+    t1 = time.perf_counter()
+    e2.run(0, P, seed)
+    e2.synchronize()
+    compute_s = time.perf_counter() - t1
+    ms0, l0, _ = e2.timing(0)
+    ms1, l1, _ = e2.timing(1)
+    diag = e2.diagnostics()
+    e2.close()
+    _, prof_b, prof_f = roofline_terms(sizes, s, True)
+    total = 3 * P * K
+    line = {
+        "metric": f"permutations/sec (whole node), {n // 1000}k genes x {len(sizes)} modules, 3 test datasets",
+        "value": total / elapsed, "unit": "permutations/sec", "n_gpus": 1, "steps": K, "warmup": W,
+        "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic coexpression (SURVEY.md 8d generator), random module layout",
+        "config": {"workload": f"C5: {n} genes x {s} samples, {len(sizes)} modules ({min(sizes)}-{max(sizes)} genes, "
+                               f"discovery over {n_disc} genes), 3 test datasets of {n} genes each in host memory, "
+                               f"null=all (pool = the {n} test genes), 7 statistics, "
+                               f"netrep_PermutationProcedure per dataset with netrep_PrefetchTestDataset",
+                   "perms_per_step": 3 * P, "perms_per_dataset_per_step": P, "parallelism": "perm-shard x1"},
+        "upload_s_per_dataset": upload_s,
+        "upload_GBps": (2 * n * n + s * n) * 8 / upload_s / 1e9,
+        "compute_s_per_dataset": compute_s,
+        "compute_perms_per_sec": P / compute_s,
+        "pipelined_s_per_dataset": elapsed / (3 * K),
+        "kernels": {"module_net_kernel": {"avg_ms": ms0 / max(l0, 1), "launches": l0},
+                    "module_profile_kernel": {"avg_ms": ms1 / max(l1, 1), "launches": l1,
+                                              "achieved": prof_f * P / (ms1 * 1e-3) / 1e12 if ms1 > 0 else None,
+                                              "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s"}},
+        "finite_fraction": finite, "setup_s": t_setup, "eigen_diagnostics": diag,
+    }
+    mk = line["kernels"]["module_profile_kernel"]
+    if mk["achieved"] is not None:
+        mk["frac"] = mk["achieved"] / mk["peak"]
+    print(json.dumps(line))
 
 
 def main():
     args = parse()
     relaunch_if_needed(args)
     world, rank, local = setup_dist(args)
+    if args.config == "C5" and not args.c5_single:
+        run_c5(args, world, rank, local)
+        return
     eng, lay, meta, tensors = build_case(args.config, world, rank, local, args.seed)
     B, K, W = args.batch, args.steps, args.warmup
     P = args.perms_per_step or max(5120, B)
@@ -392,11 +567,18 @@ def main():
             roofline["executed"] = measured_mfma(args.config, B, dom_name, dom.get("avg_ms", 0.0))
         cpu = None
         if world == 1 and not args.no_cpu_baseline and host is not None:
-            rate, dt, n_cpu, threads = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)
+            rate, dt, n_cpu, threads, hc = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)
             cpu = {"value": rate, "unit": "permutations/sec", "cores": threads, "kind": "port",
+                   "per_core": rate / threads,
+                   "host": {"cpu_model": hc["model"], "nproc": hc["nproc"], "affinity": hc["affinity"],
+                            "lease_share": hc["lease_share"],
+                            "whole_host_estimate": rate / threads * hc["nproc"],
+                            "whole_host_estimate_note": "per-core rate x nproc (linear; the reference's "
+                                                        "threads are independent, src/permutations.cpp:338-373)"},
                    "sample": f"{n_cpu} permutations x {len(lay.modules)} modules of the same workload in "
                              f"{dt:.1f} s: C++ restatement of src/permutations.cpp (std::thread chunks, "
-                             f"LAPACK SVD), {threads} threads"}
+                             f"LAPACK SVD), {threads} threads = every core of this GPU's lease "
+                             f"({hc['nproc']}-CPU host: {hc['model']})"}
         null_desc = "all" if args.config == "C5" else "overlap"
         line = {
             "metric": f"permutations/sec (whole node), {n_cfg // 1000}k genes x {len(sizes_cfg)} modules"

@@ -182,6 +182,9 @@ int nr_cancel(nr_ctx* ctx);
 
 /* Tuning and measurement. */
 int nr_set_batch(nr_ctx* ctx, int64_t perms_per_launch);
+/* Host threads of the pinned staging copies (process-wide; n <= 0: 8, the
+ * default; capped at 8). The reference-interface calls set it from n_cores. */
+int nr_set_host_threads(int n);
 int nr_set_timing(nr_ctx* ctx, int enable);
 /* Accumulated device time (HIP events on the launch stream) per kernel:
  * kernel 0 = module network statistics, 1 = summary-profile statistics. */
@@ -226,12 +229,39 @@ typedef struct netrep_disc_props {
 typedef int (*netrep_interrupt_fn)(void* user);
 void netrep_set_interrupt_hook(netrep_interrupt_fn fn, void* user);
 
+/* Progress hook: the replacement of MonitorProgress's console output
+ * (src/thread-utils.cpp:54-81: Rcpp::Rcout << endl, then "\r%5d% completed."
+ * about once a second, then endl endl). While netrep_PermutationProcedure or
+ * netrep_PermutationProcedureFiles runs with verbose != 0, the CALLING
+ * thread -- the thread R called from, so the hook may write to
+ * Rcpp::Rcout -- calls fn(event, done, total, user): NETREP_PROGRESS_BEGIN
+ * once before the first permutation, NETREP_PROGRESS_UPDATE about once a
+ * second and once more when the last permutation completes (done == total),
+ * NETREP_PROGRESS_END once after the run (also after an interrupt).
+ * netrep_format_progress renders an UPDATE exactly as the reference does.
+ * The library itself never writes to stdout or stderr (R CMD check): with no
+ * hook installed, verbose output is dropped. NULL removes the hook.
+ * Process-wide; set it before the call. */
+#define NETREP_PROGRESS_BEGIN 0
+#define NETREP_PROGRESS_UPDATE 1
+#define NETREP_PROGRESS_END 2
+typedef void (*netrep_progress_fn)(int32_t event, int64_t done, int64_t total, void* user);
+void netrep_set_progress_hook(netrep_progress_fn fn, void* user);
+/* "\r%5d% completed." with the reference's rounding
+ * ((unsigned)round((float)done / (float)total * 100), src/thread-utils.cpp:
+ * 66-68) into buf (NUL-terminated, at most cap bytes); returns the length
+ * written, or -1 if cap is too small. */
+int netrep_format_progress(int64_t done, int64_t total, char* buf, int64_t cap);
+
 /* PermutationProcedure (src/permutations.cpp:160-166) and
  * PermutationProcedureNoData (src/permutationsNoData.cpp:140-146, t_data =
  * NULL). nulls_out [n_modules x n_stat x n_perm], observed_out
  * [n_modules x n_stat], both column-major, NA-filled. `seed` keys the PRP;
- * `pi` (optional, [n_perm x n_null]) supplies explicit shuffles. n_cores is
- * accepted for interface parity; NETREP_NUM_GPUS selects the GPU count
+ * `pi` (optional, [n_perm x n_null]) supplies explicit shuffles. n_cores
+ * (nThreads of the reference, which sizes its worker pool) bounds the host
+ * threads the call uses for its own work -- the pinned staging copies of the
+ * test matrices (at most min(n_cores, 8) threads; n_cores <= 0: 8); the
+ * permutations themselves run on the GPUs. NETREP_NUM_GPUS selects the GPU count
  * (NETREP_SHARE_DEVICE=1 lets several contexts share the visible GPUs, a test
  * mode for the sharded path on a one-GPU machine). The test matrices are
  * uploaded once, to the first GPU, and copied device to device to the others.
@@ -267,13 +297,19 @@ void netrep_DiscardPrefetch(void);
  * (R/disk-matrix-class.R; the R code would otherwise loadIntoRAM() them,
  * R/modulePreservation.R:553-620): the files go straight to GPU 0's HBM,
  * tData is scaled there, and the node names are the network file's column
- * names. Other arguments and outputs as netrep_PermutationProcedure. */
+ * names. The three files must agree on the node order: the correlation,
+ * network and data files' column names (and the square matrices' row names)
+ * must be identical where present, as R/check-user-input.R:757-771 requires
+ * ("mismatch in node order between data, correlation, and network"). pi_len
+ * is the number of entries in pi (n_perm x n_null, checked once the node
+ * names -- hence n_null -- are known; -1: unchecked). Other arguments and
+ * outputs as netrep_PermutationProcedure. */
 int netrep_PermutationProcedureFiles(const netrep_disc_props* disc_props, const char* t_data_file,
                                      const char* t_corr_file, const char* t_net_file,
                                      const char* const* ma_names, const char* const* ma_labels,
                                      int64_t n_assign, const char* const* modules, int64_t n_modules,
                                      int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
-                                     int32_t verbose, uint64_t seed, const uint32_t* pi,
+                                     int32_t verbose, uint64_t seed, const uint32_t* pi, int64_t pi_len,
                                      double* nulls_out, double* observed_out);
 
 /* Host read of one numeric matrix from an RDS file or save() archive (the

@@ -11,8 +11,10 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# NETREP_LIB: another in-tree build of the same library (A/B runs of compile-time variants)
-LIB_PATH = os.environ.get("NETREP_LIB") or os.path.join(_HERE, "_lib", "libnetrep_amd.so")
+# The in-tree build. A/B tools (tools/probes/profile_ab.py) point LIB_PATH at
+# another build of the same library before the first load(); no environment
+# variable selects the library or anything inside it.
+LIB_PATH = os.path.join(_HERE, "_lib", "libnetrep_amd.so")
 
 NR_OK = 0
 NR_ERR_HIP = 1
@@ -43,6 +45,8 @@ _u32p = C.POINTER(C.c_uint32)
 _intp = C.POINTER(C.c_int)
 _strv = C.POINTER(C.c_char_p)
 INTERRUPT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p)   # netrep_interrupt_fn
+PROGRESS_FN = C.CFUNCTYPE(None, C.c_int32, C.c_int64, C.c_int64, C.c_void_p)  # netrep_progress_fn
+PROGRESS_BEGIN, PROGRESS_UPDATE, PROGRESS_END = 0, 1, 2
 
 
 class DiscProps(C.Structure):
@@ -94,6 +98,9 @@ SIGNATURES = {
     "netrep_CheckFinite": (_int, [_dp, _i64, _i64]),
     "netrep_last_error": (C.c_char_p, []),
     "netrep_set_interrupt_hook": (None, [C.c_void_p, C.c_void_p]),
+    "netrep_set_progress_hook": (None, [C.c_void_p, C.c_void_p]),
+    "netrep_format_progress": (_int, [_i64, _i64, C.c_char_p, _i64]),
+    "nr_set_host_threads": (_int, [_int]),
     "netrep_PrefetchTestDataset": (_int, [_dp, _dp, _dp, _i64, _i64]),
     "nr_set_dataset_files": (_int, [_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
                                     C.c_char_p, _int]),
@@ -101,7 +108,7 @@ SIGNATURES = {
     "nr_dataset_colnames": (_int, [_p, C.c_char_p, _i64, _i64p]),
     "netrep_PermutationProcedureFiles": (_int, [C.POINTER(DiscProps), C.c_char_p, C.c_char_p, C.c_char_p,
                                                 _strv, _strv, _i64, _strv, _i64, _i64, _i32, C.c_char_p,
-                                                _i32, _u64, _u32p, _dp, _dp]),
+                                                _i32, _u64, _u32p, _i64, _dp, _dp]),
     "netrep_ReadRDSMatrix": (_int, [C.c_char_p, C.c_char_p, _i64p, _i64p, _dp, C.c_char_p, _i64, _i64p]),
     "netrep_DiscardPrefetch": (None, []),
 }

@@ -20,6 +20,7 @@ computed on the CPU.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 from dataclasses import dataclass
 from typing import Mapping, Optional, Sequence
 
@@ -174,6 +175,52 @@ def set_interrupt_hook(fn) -> None:
     lib.netrep_set_interrupt_hook(C.cast(cb, C.c_void_p), None)
 
 
+_progress_keep = None
+_progress_user_set = False
+
+
+def format_progress(done: int, total: int) -> str:
+    """MonitorProgress's line, "\\r%5d% completed." (src/thread-utils.cpp:66-68),
+    rendered by the library (netrep_format_progress)."""
+    buf = C.create_string_buffer(64)
+    n = L.load().netrep_format_progress(int(done), int(total), buf, 64)
+    return buf.value.decode() if n >= 0 else ""
+
+
+def _install_progress(fn) -> None:
+    global _progress_keep
+    lib = L.load()
+    if fn is None:
+        lib.netrep_set_progress_hook(None, None)
+        _progress_keep = None
+        return
+    cb = L.PROGRESS_FN(lambda ev, done, total, _user: fn(int(ev), int(done), int(total)))
+    _progress_keep = cb
+    lib.netrep_set_progress_hook(C.cast(cb, C.c_void_p), None)
+
+
+def set_progress_hook(fn) -> None:
+    """Install ``fn(event, done, total)`` as the progress report of a verbose
+    PermutationProcedure (netrep_set_progress_hook; event 0 begin, 1 update
+    about once a second, 2 end) -- MonitorProgress's console output
+    (src/thread-utils.cpp:54-81). ``None`` restores the default, which prints
+    the reference's lines to ``sys.stdout``; the library itself never writes
+    to stdout."""
+    global _progress_user_set
+    _progress_user_set = fn is not None
+    _install_progress(fn)
+
+
+def _print_progress(ev: int, done: int, total: int) -> None:
+    if ev == L.PROGRESS_BEGIN:
+        sys.stdout.write("\n")
+    elif ev == L.PROGRESS_UPDATE:
+        sys.stdout.write(format_progress(done, total))
+    else:
+        sys.stdout.write("\n\n")
+    sys.stdout.flush()
+
+
 # Datasets handed to netrep_PrefetchTestDataset: their column-major arrays
 # stay referenced here until the PermutationProcedure call that adopts them
 # (at most two pending, as in the library).
@@ -259,6 +306,8 @@ def _permutation(disc_props, t_data, t_corr, t_net, module_assignments, modules,
     an, _k2 = _strv(names)
     al, _k3 = _strv(labels)
     mo, _k4 = _strv(modules)
+    if verbose and not _progress_user_set:
+        _install_progress(_print_progress)  # the reference's console lines, from Python
     rc = lib.netrep_PermutationProcedure(
         C.byref(dp), _dptr(data), _dptr(corr), _dptr(net), s, n, tn, an, al, len(names), mo, nm_,
         int(n_perm), int(n_cores), str(null_hypothesis).encode(), int(bool(verbose)),
@@ -350,11 +399,17 @@ def PermutationProcedureFiles(discProps: dict, tData_file: Optional[str], tCorr_
     al, _k3 = _strv(labels)
     mo, _k4 = _strv(modules)
     enc = lambda x: None if x is None else str(x).encode()  # noqa: E731
+    if pi_arr is not None and (pi_arr.ndim != 2 or pi_arr.shape[0] != int(nPermutations)):
+        raise L.NetRepError(L.NR_ERR_INVALID, f"pi must have shape (nPermutations, n_null), got {pi_arr.shape}")
+    if verbose and not _progress_user_set:
+        _install_progress(_print_progress)
+    # n_null is known only once the files' node names are read: the library
+    # checks pi's length against it (pi_len)
     rc = lib.netrep_PermutationProcedureFiles(
         C.byref(dp), enc(tData_file), enc(tCorr_file), enc(tNet_file), an, al, len(names), mo, nm_,
         int(nPermutations), int(nCores), str(nullHypothesis).encode(), int(bool(verbose)),
         int(seed) & (2**64 - 1), pi_arr.ctypes.data_as(C.POINTER(C.c_uint32)) if pi_arr is not None else None,
-        _dptr(nulls), _dptr(observed))
+        int(pi_arr.size) if pi_arr is not None else -1, _dptr(nulls), _dptr(observed))
     interrupted = rc == L.NR_ERR_CANCELLED
     if not interrupted:
         L.check_api(rc)

@@ -437,7 +437,7 @@ struct LzLds {
 
 // Carves red, q, qprev, w, vv, gv, colm (kvec each), then `extra` doubles for
 // the storage scheme (returned in *extra_out), then the Lanczos tridiagonal
-// arrays and idx. Layout matches profile_kernel_lds / reg_kernel_lds.
+// arrays and idx. Layout matches profile_kernel_lds.
 template <int NW>
 __device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mmax, int64_t extra,
                                            double** extra_out, bool twork_in_extra = false) {

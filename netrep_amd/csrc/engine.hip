@@ -39,13 +39,6 @@ struct DeviceTimer {
 struct nr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  // NETREP_CONCURRENT=1 runs the gather (network) kernel on `side`,
-  // concurrently with the summary-profile kernel. Off by default: measured
-  // at C3 it costs 14% (6,090 vs 7,077 perms/s) because the gather kernel's
-  // workgroups take CU slots from the persistent profile grid.
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  bool concurrent = false;
   std::string err;
   std::mutex mu;
 
@@ -54,6 +47,9 @@ struct nr_ctx {
   double* d_data = nullptr;
   int64_t n_nodes = 0, n_samples = 0;
   std::vector<std::string> node_names;  // column names of a dataset loaded from files
+  int64_t data_gen = 0;                 // bumped by every dataset change (reset_dataset)
+  int64_t modules_gen = -1;             // data_gen the modules were validated against
+  int64_t null_gen = -1;                // data_gen the null pool was validated against
   int symmetric = 0;
   int corr_finite = 0, net_finite = 0;  // CheckFinite of the resident matrices
 
@@ -185,6 +181,20 @@ int fill_na(nr_ctx* ctx, double* d, int64_t n) {
 
 int n_stat_of(const nr_ctx* ctx) { return ctx->d_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA; }
 
+// No dataset: buffers freed, shape zero. Modules validated against an earlier
+// dataset (their node indices) stop being usable: check_ready demands a new
+// nr_set_modules after any dataset change.
+void reset_dataset(nr_ctx* ctx) {
+  dfree(ctx->d_pairs);
+  dfree(ctx->d_data);
+  ctx->node_names.clear();
+  ctx->n_nodes = 0;
+  ctx->n_samples = 0;
+  ctx->symmetric = 0;
+  ctx->corr_finite = ctx->net_finite = 0;
+  ++ctx->data_gen;
+}
+
 // Lanczos basis columns per item: 160 covers every C2/C3 module (<= 46 steps
 // measured); large modules (C5: up to 2,000 nodes, spectra with small gaps)
 // get 320.
@@ -193,25 +203,22 @@ int profile_m_max(int k_max) { return k_max <= 320 ? std::min(k_max, 160) : 320;
 // padded to a 32-column super-tile.
 int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
 
-// Launch plan of the summary-profile kernel. Default: the packed symmetric
-// Gram in global scratch, 4-wave workgroups, 3 per CU (variant 2; measured
-// fastest at C3: 23.2 ms per 256 permutations). Alternatives for A/B: the
-// register-resident 4-wave kernel for modules of <= 255 nodes (variant 5,
-// kernels_rg4.hip; larger modules of the same launch go to variant 2),
-// the register-resident Gram (variant 3, one 8-wave workgroup per CU, the
-// Gram never leaves the registers/LDS of the CU that computed it; modules of
-// <= 303 nodes; 30.5 ms), packed 8-wave (1) and full Gram (0, also the
-// fallback when the packed layout does not fit LDS):
-// NETREP_PROFILE_VARIANT=rg4|reg|packed4|packed|full, NETREP_PROFILE_WG_PER_CU
-// (a non-rg4 value applies to every module).
+// Launch plan of one summary-profile launch (one size class of modules):
+//   variant 2: the packed symmetric Gram in global scratch, 4-wave
+//              workgroups, 3 per CU (module_profile_packed4_kernel; the
+//              compile-time LDS layout of 320-node modules, or a runtime one);
+//   variant 0: the full Gram, where the packed layout's LDS does not fit;
+//   variant 4: the full Gram with the matvec partials in scratch, where even
+//              that does not fit; `big`: the per-node arrays in scratch too
+//              (modules beyond the LDS vectors; dual Gram only).
+// Modules with k > S use the S x S dual Gram. One numerical path per layout:
+// no run-time switch selects another (round-2 A/B variants are compile-time
+// history, profiles/r02/profile_variants.txt and profiles/r03/).
 struct ProfilePlan {
-  int variant = 0;  // 0 full Gram, 1 packed 8-wave, 2 packed 4-wave, 3 register-resident (8 waves),
-                    // 4 full Gram with the matvec partials in global scratch (large modules),
-                    // 5 register-resident 4-wave (kernels_rg4.hip, the default for k <= 303)
+  int variant = 0;
   int slots = 0;
   int per_cu = 1;
   int64_t gram_doubles = 0, stride = 0;
-  bool dual = false;  // S x S Gram for the modules with k > S
   int k_gram = 0;     // side of the largest Gram (minus the ones column)
   int m = 0;          // Lanczos basis columns
   int kvec = 0;       // LDS vector length
@@ -219,51 +226,6 @@ struct ProfilePlan {
   int64_t basis_doubles = 0;
   int64_t g32_off = 0;  // fp32 Gram copy (relaxed Lanczos steps), 0: none
 };
-
-// Opt-in (NETREP_FUSE=1): measured on C3 the fused kernel takes 24.77 ms per
-// 256-permutation launch against 20.73 + 4.21 ms for the two launches, a 0.7%
-// gain inside run-to-run noise (profiles/r02/profile_variants.txt), so the
-// default keeps the kernels separate and each one's roofline readable.
-bool fuse_enabled() {
-  const char* f = std::getenv("NETREP_FUSE");
-  return f && f[0] == '1';
-}
-
-// The S x S (dual) Gram for modules larger than the sample count; on unless
-// NETREP_DUAL_GRAM=0 (A/B runs).
-bool dual_gram_enabled() {
-  const char* f = std::getenv("NETREP_DUAL_GRAM");
-  return !(f && f[0] == '0');
-}
-
-// Relaxed Lanczos steps on an fp32 copy of the packed Gram once the residual
-// is below 1e-7 theta (kernels.hip lanczos_ritz); on unless NETREP_RELAX=0.
-bool relax_enabled() {
-  const char* f = std::getenv("NETREP_RELAX");
-  return !(f && f[0] == '0');
-}
-
-// Lanczos start vector: the Gram column of largest norm (kernels.hip
-// start_column); on unless NETREP_START_COL=0 (A/B runs).
-bool start_col_enabled() {
-  const char* f = std::getenv("NETREP_START_COL");
-  return !(f && f[0] == '0');
-}
-
-// G v of the Ritz vector from the Lanczos relation (kernels.hip lanczos_ritz);
-// on unless NETREP_GV_RELATION=0 (A/B runs).
-bool gv_relation_enabled() {
-  const char* f = std::getenv("NETREP_GV_RELATION");
-  return !(f && f[0] == '0');
-}
-
-// NETREP_PROFILE_VARIANT (A/B runs): -1 when unset.
-int profile_variant_env() {
-  const char* f = std::getenv("NETREP_PROFILE_VARIANT");
-  if (!f) return -1;
-  const std::string v(f);
-  return v == "packed" ? 1 : v == "full" ? 0 : v == "reg" ? 3 : v == "packed4" ? 2 : v == "rg4" ? 5 : -1;
-}
 
 // Queue order of the summary-profile items. Module-major (every permutation
 // of the largest module, then the next: largest-first scheduling) balances
@@ -277,18 +239,15 @@ int profile_variant_env() {
 // working set would overflow the cache budget and the mix fits it (C3:
 // 18.75 -> 18.17 ms); with Grams that overflow it either way (C5, S = 1000:
 // 445 vs 387 ms module-major) or fit it either way (C2), module-major.
-// NETREP_PROFILE_ORDER_TAIL=0 forces module-major order, any other value
-// permutation-major with that T.
 int profile_order_tail(int slots, const std::vector<int32_t>& k_sorted, int first, int n_mod, int64_t n_perm,
-                       int n_samples, bool dual) {
-  if (const char* e = std::getenv("NETREP_PROFILE_ORDER_TAIL")) return std::max(0, std::atoi(e));
+                       int n_samples) {
   if (n_mod <= 1) return 0;
   const int64_t t = (slots + n_mod - 1) / n_mod;
   if (t >= n_perm) return 0;
   // per-slot working set of a module: packed Gram (+ its fp32 copy) and a
   // ~40-column Lanczos basis of the Gram's side
   auto live = [&](int k) {
-    const int side = dual ? std::min(k, n_samples) : k;
+    const int side = std::min(k, n_samples);
     return (double)nr::packed_gram_doubles(side + 1) * 12.0 + 40.0 * 8.0 * side;
   };
   double mix = 0.0;
@@ -305,30 +264,17 @@ int profile_order_tail(int slots, const std::vector<int32_t>& k_sorted, int firs
   return (top > budget && mix <= budget) ? (int)t : 0;
 }
 
-// rg4: plan the register-resident 4-wave kernel (variant 5; the caller
-// guarantees k_max <= rg4_kernel_k_max()).
-int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg4, ProfilePlan* plan) {
+int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, ProfilePlan* plan) {
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-  if (rg4) {
-    plan->variant = 5;
-    plan->per_cu = 1;
-    plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, dev_cu));
-    plan->gram_doubles = 0;  // the Gram lives in registers / LDS
-    plan->stride = (int64_t)nr::kRg4StepCap * k_max;  // Lanczos basis columns beyond the LDS share
-    return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
-  }
-  const int forced = profile_variant_env();
-  int variant = forced >= 0 && forced != 5 ? forced : 2;
+  int variant = 2;
   // the dual (S x S) Gram of modules with k > S: the Gram side is min(k, S),
   // and so is every Lanczos dimension (basis columns of that length)
-  plan->dual = dual_gram_enabled() && variant != 3;
-  plan->k_gram = plan->dual ? std::min(k_max, n_samples) : k_max;
+  plan->k_gram = std::min(k_max, n_samples);
   const int mg = profile_m_max(plan->k_gram);
   plan->m = mg;
   int kvec = k_max;
-  if (variant == 3 && k_max > nr::reg_kernel_k_max()) variant = 2;
-  if (variant != 0 && nr::profile_kernel_lds(kvec, mg, n_samples, variant) > 160 * 1024) variant = 0;
+  if (nr::profile_kernel_lds(kvec, mg, n_samples, 2) > 160 * 1024) variant = 0;
   // Large modules: the per-wave matvec partials (4 x k doubles) move from LDS
   // to the slot's scratch, which leaves LDS for the six Lanczos vectors only.
   if (variant == 0 && nr::profile_kernel_lds(kvec, mg, n_samples, 0) > 160 * 1024) variant = 4;
@@ -338,7 +284,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
   plan->big = false;
   if (variant == 4 && nr::profile_kernel_lds(kvec, mg, n_samples, 4) > 160 * 1024) {
     kvec = nr::profile_kvec_max(mg);
-    if (!plan->dual || n_samples > kvec)
+    if (n_samples > kvec)
       return fail(ctx, NR_ERR_UNSUPPORTED,
                   "module of more than " + std::to_string(kvec) + " nodes needs the dual Gram and at most " +
                       std::to_string(kvec) + " samples");
@@ -348,18 +294,12 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
   const size_t lds = nr::profile_kernel_lds(kvec, mg, n_samples, variant);
   if (lds > 160 * 1024)
     return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
-  int want = variant == 1 ? 2 : 3;
-  if (const char* e = std::getenv("NETREP_PROFILE_WG_PER_CU")) want = std::max(1, std::min(4, std::atoi(e)));
-  if (variant == 1) want = std::min(want, 2);
-  if (variant == 2) want = std::max(2, want);
-  if (variant == 3 || variant == 4) want = 1;
+  const int want = variant == 4 ? 1 : 3;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
   plan->variant = variant;
   plan->per_cu = per_cu;
   plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * per_cu));
-  if (variant == 3) {
-    plan->gram_doubles = 0;  // the Gram lives in registers and LDS
-  } else if (variant == 1 || variant == 2) {
+  if (variant == 2) {
     const int64_t kc = plan->k_gram + 1;
     plan->gram_doubles = nr::packed_gram_doubles((int)kc);  // packed triangle in chunked column groups
   } else {
@@ -371,31 +311,26 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, bool rg
                  (variant == 4 ? (int64_t)nr::kProfileWaves * kvec : 0) +
                  (plan->big ? 5 * (int64_t)k_max : 0);  // x.u, means, squares, contributions, index set
   plan->g32_off = 0;
-  if ((variant == 1 || variant == 2) && relax_enabled()) {  // fp32 copy of the packed Gram at the slot's end
+  if (variant == 2) {  // fp32 copy of the packed Gram at the slot's end (relaxed Lanczos steps)
     plan->stride = (plan->stride + 31) / 32 * 32;
     plan->g32_off = plan->stride;
     plan->stride += (plan->gram_doubles / 2 + 31) / 32 * 32;
   }
-  return ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)(plan->stride * plan->slots));
+  return NR_OK;
 }
 
-// Summary-profile launches over a module order sorted by size (descending,
-// k_sorted[i] = size of d_order[i]): the modules above rg4_kernel_k_max() run
-// first on the scratch-Gram variants, the rest as one register-resident
-// (variant 5) launch, each launch with its own work queue and k_max.
+// Summary-profile launches over the module order sorted by size (descending,
+// k_sorted[i] = size of d_order[i]), one per size class, each with its own
+// work queue, k_max and layout: the modules beyond the packed kernel's
+// compile-time 320-node layout first (full or runtime-layout Gram), then the
+// rest on the packed kernel at 3 workgroups per CU. (Round 2 launched every
+// module on the layout of the largest one: at C5 the small modules ran on the
+// one-workgroup-per-CU full-Gram kernel too.)
 int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
                     const std::vector<int32_t>& k_sorted, int64_t n_perm, hipStream_t st) {
   const int n_mod = (int)k_sorted.size();
-  const int forced = profile_variant_env();
-  // The register-resident kernel is opt-in (NETREP_PROFILE_VARIANT=rg4): one
-  // wave per SIMD leaves its latency chains exposed and it measured 1.45x
-  // slower than packed4 on C3's <= 255-node modules (24.4 vs 16.7 ms per 256
-  // permutations; profiles/r02/profile_variants.txt).
-  int n_big = n_mod;
-  if (forced == 5) {
-    n_big = 0;
-    while (n_big < n_mod && k_sorted[n_big] > nr::rg4_kernel_k_max()) ++n_big;
-  }
+  int n_big = 0;
+  while (n_big < n_mod && k_sorted[n_big] > nr::kPackedLayoutK) ++n_big;
   struct Seg {
     int first, count;
     ProfilePlan plan;
@@ -403,36 +338,34 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
   int ns = 0;
   if (n_big > 0) seg[ns++] = {0, n_big, {}};
   if (n_big < n_mod) seg[ns++] = {n_big, n_mod - n_big, {}};
+  // every segment's scratch (slots x stride) is one allocation, carved in turn
+  int64_t total = 0;
   for (int i = 0; i < ns; ++i) {
     const int rc = plan_profile(ctx, (int64_t)seg[i].count * n_perm, k_sorted[seg[i].first], (int)pp.n_samples,
-                                seg[i].first == n_big, &seg[i].plan);
+                                &seg[i].plan);
     if (rc) return rc;
+    total = std::max<int64_t>(total, seg[i].plan.stride * seg[i].plan.slots);
   }
-  for (int i = 0; i < ns; ++i) {  // scratch final after every plan
+  // segments run one after the other on one stream: they share the scratch
+  if (int rc = ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)total)) return rc;
+  for (int i = 0; i < ns; ++i) {
     const ProfilePlan& plan = seg[i].plan;
     const int k_max = k_sorted[seg[i].first];
     pp.mod_order = d_order + seg[i].first;
     pp.n_items = (int32_t)((int64_t)seg[i].count * n_perm);
     pp.k_max = k_max;
-    pp.ld = gram_ld(plan.variant == 5 ? k_max : plan.k_gram);
-    pp.m_max = plan.variant == 5 ? profile_m_max(k_max) : plan.m;
-    pp.dual = plan.dual ? 1 : 0;
-    pp.kvec = plan.variant == 5 ? 0 : plan.kvec;
+    pp.ld = gram_ld(plan.k_gram);
+    pp.m_max = plan.m;
+    pp.kvec = plan.kvec;
     pp.basis_doubles = plan.basis_doubles;
     pp.gram_doubles = plan.gram_doubles;
     pp.scratch = ctx->d_scratch;
     pp.scratch_stride = plan.stride;
     pp.part_global = plan.variant == 4 ? 1 : 0;
-    pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples,
-                                       plan.dual);
-    pp.g32_off = plan.variant == 5 ? 0 : plan.g32_off;
-    pp.start_col = start_col_enabled() ? 1 : 0;
-    pp.gv_relation = gv_relation_enabled() ? 1 : 0;
+    pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples);
+    pp.g32_off = plan.g32_off;
     NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
-    if (plan.variant == 5)
-      NR_HIP(ctx, nr::launch_profile_rg4(pp, plan.slots, st));
-    else
-      NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, st));
+    NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, st));
   }
   return NR_OK;
 }
@@ -548,24 +481,13 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   np.slot_cor_degree = data ? 3 : 2;
   np.slot_avg_cor = data ? 5 : 3;
   np.out = d_out;
-  // NETREP_FUSE=1: the network statistics ride in the summary-profile
-  // kernel's item pipeline when every module fits its LDS layout (<= 320
-  // nodes), in the Lanczos vectors' LDS before each item's Gram.
-  // Otherwise (the default: NETREP_FUSE unset) they are their own launch
-  // (module_net_kernel) ahead of the summary-profile kernel;
-  // NETREP_CONCURRENT=1 puts that launch on the side stream.
-  const bool fuse = data && ctx->k_max <= 320 && profile_variant_env() < 0 && fuse_enabled();
-  const bool fork = data && !fuse && ctx->concurrent;
-  hipStream_t net_stream = fork ? ctx->side : ctx->stream;
-  if (fork) {
-    NR_HIP(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
-    NR_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-  }
-  if (!fuse) {
-    timer_begin(ctx, 0, net_stream);
-    if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ctx->order_k_h, n_perm, net_stream))) return rc;
-    timer_end(ctx, 0, n_items, net_stream);
-  }
+  // The network statistics are their own launch (module_net_kernel) ahead of
+  // the summary-profile launches, on the same stream. (Round 2 measured the
+  // network phase fused into the profile items at +0.7%, within run-to-run
+  // noise, and on a concurrent stream at -11%: profiles/r02/profile_variants.txt.)
+  timer_begin(ctx, 0, ctx->stream);
+  if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ctx->order_k_h, n_perm, ctx->stream))) return rc;
+  timer_end(ctx, 0, n_items, ctx->stream);
 
   if (data) {
     nr::ProfileParams pp{};
@@ -586,16 +508,10 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.queue = ctx->d_counters;
     pp.diag = ctx->d_counters + 1;
     pp.stamps = ctx->d_stamps;
-    pp.fuse_net = fuse ? 1 : 0;
-    pp.net = np;
     timer_begin(ctx, 1, ctx->stream);
     rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ctx->stream);
     if (rc) return rc;
     timer_end(ctx, 1, n_items, ctx->stream);
-  }
-  if (fork) {
-    NR_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
-    NR_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
   }
   timer_collect(ctx);
   return NR_OK;
@@ -627,8 +543,12 @@ int64_t auto_batch(const nr_ctx* ctx) {
 int check_ready(nr_ctx* ctx, bool need_null) {
   if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset: call nr_set_dataset first");
   if (ctx->n_rows <= 0) return fail(ctx, NR_ERR_INVALID, "no modules: call nr_set_modules first");
+  if (ctx->modules_gen != ctx->data_gen)
+    return fail(ctx, NR_ERR_INVALID, "the modules were set for another dataset: call nr_set_modules again");
   if (need_null && ctx->n_present > 0 && (!ctx->d_null_idx || !ctx->d_null_pos))
     return fail(ctx, NR_ERR_INVALID, "no null pool: call nr_set_null_pool and pass null_pos");
+  if (need_null && ctx->n_present > 0 && ctx->null_gen != ctx->data_gen)
+    return fail(ctx, NR_ERR_INVALID, "the null pool was set for another dataset: call nr_set_null_pool again");
   // Every permuted index is null_idx[pi(null_pos)]: a position outside the pool
   // would be read out of bounds on the device.
   if (need_null && ctx->n_present > 0 && ctx->null_pos_max >= ctx->n_null)
@@ -773,10 +693,6 @@ int nr_ctx_create(int device, nr_ctx** out) {
   ctx->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
-  if (const char* c = std::getenv("NETREP_CONCURRENT")) ctx->concurrent = std::atoi(c) != 0;
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, 16 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, 16 * sizeof(int));
@@ -793,7 +709,6 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   dfree(ctx->d_pairs);
   dfree(ctx->d_data);
   dfree(ctx->d_row_of);
@@ -816,9 +731,6 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   for (auto& ev : ctx->ev)
     if (ev) (void)hipEventDestroy(ev);
-  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -827,10 +739,19 @@ const char* nr_last_error(const nr_ctx* ctx) {
   return ctx ? ctx->err.c_str() : g_create_error.c_str();
 }
 
-// Copy n doubles with up to 8 host threads (pageable -> pinned staging).
+// Host threads of the staging copies (nr_set_host_threads; the reference
+// interface passes nCores).
+static std::atomic<int> g_host_threads{8};
+
+int nr_set_host_threads(int n) {
+  g_host_threads = n <= 0 ? 8 : std::min(n, 8);
+  return NR_OK;
+}
+
+// Copy n doubles with up to g_host_threads host threads (pageable -> pinned staging).
 static void parallel_copy(double* dst, const double* src, int64_t n) {
   const int64_t min_part = (int64_t)1 << 20;  // 8 MiB per thread at least
-  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(8, n / min_part));
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(g_host_threads.load(), n / min_part));
   if (nt == 1) {
     std::memcpy(dst, src, (size_t)n * sizeof(double));
     return;
@@ -888,6 +809,11 @@ static int upload_pinned(nr_ctx* ctx, const double* corr, const double* net, int
   return NR_OK;
 }
 
+namespace {
+int set_dataset_impl(nr_ctx* ctx, const double* corr, const double* net, const double* data,
+                     int64_t n_nodes, int64_t n_samples, int where);
+}
+
 int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const double* data,
                    int64_t n_nodes, int64_t n_samples, int where) {
   if (!ctx) return NR_ERR_INVALID;
@@ -896,11 +822,18 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   if (n_nodes > (int64_t)INT32_MAX) return fail(ctx, NR_ERR_UNSUPPORTED, "n_nodes exceeds 2^31-1");
   NR_HIP(ctx, hipSetDevice(ctx->device));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  dfree(ctx->d_pairs);
-  dfree(ctx->d_data);
-  ctx->node_names.clear();
-  ctx->n_nodes = n_nodes;
-  ctx->n_samples = data ? n_samples : 0;
+  reset_dataset(ctx);
+  const int rc = set_dataset_impl(ctx, corr, net, data, n_nodes, n_samples, where);
+  if (rc != NR_OK) {
+    (void)hipStreamSynchronize(ctx->stream);
+    reset_dataset(ctx);
+  }
+  return rc;
+}
+
+namespace {
+int set_dataset_impl(nr_ctx* ctx, const double* corr, const double* net, const double* data,
+                     int64_t n_nodes, int64_t n_samples, int where) {
   const int64_t n_elem = n_nodes * n_nodes;
   NR_HIP(ctx, hipMalloc((void**)&ctx->d_pairs, (size_t)n_elem * sizeof(double2)));
   if (where == NR_DEVICE) {
@@ -928,8 +861,11 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
   ctx->symmetric = (asym & 1) ? 0 : 1;
   ctx->corr_finite = (asym & 2) ? 0 : 1;
   ctx->net_finite = (asym & 4) ? 0 : 1;
+  ctx->n_nodes = n_nodes;
+  ctx->n_samples = data ? n_samples : 0;
   return NR_OK;
 }
+}  // namespace
 
 // File -> pinned -> HBM for one matrix payload: the host inflates / reads
 // straight into pinned buffer b while the copy engine moves the previous one
@@ -972,13 +908,10 @@ static int upload_file_matrix(nr_ctx* ctx, nr::RMatrixReader& rd, double2* pairs
   return NR_OK;
 }
 
-int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_path, const char* data_path,
-                         const char* corr_object, const char* net_object, const char* data_object,
-                         int scale_data) {
-  if (!ctx) return NR_ERR_INVALID;
-  if (!corr_path || !net_path) return fail(ctx, NR_ERR_INVALID, "corr/net file missing");
-  NR_HIP(ctx, hipSetDevice(ctx->device));
-  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+namespace {
+int set_dataset_files_impl(nr_ctx* ctx, const char* corr_path, const char* net_path, const char* data_path,
+                           const char* corr_object, const char* net_object, const char* data_object,
+                           int scale_data) {
   nr::RMatrixReader rc_, rn_;
   if (!rc_.open(corr_path, corr_object)) return fail(ctx, NR_ERR_INVALID, std::string(corr_path) + ": " + rc_.error());
   if (!rn_.open(net_path, net_object)) return fail(ctx, NR_ERR_INVALID, std::string(net_path) + ": " + rn_.error());
@@ -987,9 +920,6 @@ int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_pat
   if (n_nodes <= 0 || n_nodes * n_nodes != n_elem) return fail(ctx, NR_ERR_INVALID, "correlation matrix is not square");
   if (rn_.length() != n_elem) return fail(ctx, NR_ERR_INVALID, "network and correlation matrices differ in size");
   if (n_nodes > (int64_t)INT32_MAX) return fail(ctx, NR_ERR_UNSUPPORTED, "n_nodes exceeds 2^31-1");
-  dfree(ctx->d_pairs);
-  dfree(ctx->d_data);
-  ctx->node_names.clear();
   NR_HIP(ctx, hipMalloc((void**)&ctx->d_pairs, (size_t)n_elem * sizeof(double2)));
   int rc;
   nr::RMatrixMeta mc, mn;
@@ -999,7 +929,14 @@ int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_pat
   if (!rn_.finish(&mn)) return fail(ctx, NR_ERR_INVALID, std::string(net_path) + ": " + rn_.error());
   if (mc.nrow != n_nodes || mc.ncol != n_nodes || mn.nrow != n_nodes || mn.ncol != n_nodes)
     return fail(ctx, NR_ERR_INVALID, "correlation / network matrices must be square and of one size");
-  ctx->node_names = !mn.colnames.empty() ? mn.colnames : mc.colnames;
+  // R/check-user-input.R:750-771: row and column names of each square matrix
+  // agree, and the node order is the same in correlation, network and data
+  if ((!mc.rownames.empty() && !mc.colnames.empty() && mc.rownames != mc.colnames) ||
+      (!mn.rownames.empty() && !mn.colnames.empty() && mn.rownames != mn.colnames))
+    return fail(ctx, NR_ERR_INVALID, "mismatch between row and column names in 'correlation' / 'network'");
+  if (!mc.colnames.empty() && !mn.colnames.empty() && mc.colnames != mn.colnames)
+    return fail(ctx, NR_ERR_INVALID, "mismatch in node order between 'data', 'correlation', and 'network'");
+  const std::vector<std::string> names = !mn.colnames.empty() ? mn.colnames : mc.colnames;
   int64_t n_samples = 0;
   if (data_path) {
     nr::RMatrixReader rd;
@@ -1014,6 +951,8 @@ int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_pat
     if (!rc && !rd.finish(&md)) rc = fail(ctx, NR_ERR_INVALID, std::string(data_path) + ": " + rd.error());
     if (!rc && (md.nrow != n_samples || md.ncol != n_nodes))
       rc = fail(ctx, NR_ERR_INVALID, "data matrix must be samples x nodes");
+    if (!rc && !md.colnames.empty() && !names.empty() && md.colnames != names)
+      rc = fail(ctx, NR_ERR_INVALID, "mismatch in node order between 'data', 'correlation', and 'network'");
     hipError_t e = hipSuccess;
     if (!rc) e = hipMalloc((void**)&ctx->d_data, (size_t)(n_samples * (n_nodes + 2)) * sizeof(double));
     // Scale (src/scale.cpp:14-25) on the device, as the R code scales after loading
@@ -1025,12 +964,8 @@ int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_pat
     (void)hipFree(raw);
     if (rc) return rc;
     if (e != hipSuccess) return hip_fail(ctx, e, "data upload");
-    ctx->n_samples = n_samples;
-    ctx->n_nodes = n_nodes;
     if ((rc = fill_virtual_columns(ctx, n_nodes, n_samples))) return rc;
   }
-  ctx->n_nodes = n_nodes;
-  ctx->n_samples = n_samples;
   NR_HIP(ctx, hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream));
   NR_HIP(ctx, nr::launch_symmetry(ctx->d_pairs, n_nodes, ctx->d_counters + 5, ctx->stream));
   int asym = 0;
@@ -1039,7 +974,39 @@ int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_pat
   ctx->symmetric = (asym & 1) ? 0 : 1;
   ctx->corr_finite = (asym & 2) ? 0 : 1;
   ctx->net_finite = (asym & 4) ? 0 : 1;
+  // committed only once everything above has succeeded
+  ctx->node_names = names;
+  ctx->n_nodes = n_nodes;
+  ctx->n_samples = n_samples;
   return NR_OK;
+}
+}  // namespace
+
+int nr_set_dataset_files(nr_ctx* ctx, const char* corr_path, const char* net_path, const char* data_path,
+                         const char* corr_object, const char* net_object, const char* data_object,
+                         int scale_data) {
+  if (!ctx) return NR_ERR_INVALID;
+  if (!corr_path || !net_path) return fail(ctx, NR_ERR_INVALID, "corr/net file missing");
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // The old dataset is dropped first; on any failure the context is left with
+  // no dataset at all (never a new buffer with the old shape), and modules
+  // set for the old dataset are invalidated either way.
+  reset_dataset(ctx);
+  int rc;
+  try {
+    rc = set_dataset_files_impl(ctx, corr_path, net_path, data_path, corr_object, net_object, data_object,
+                                scale_data);
+  } catch (const std::bad_alloc&) {
+    rc = fail(ctx, NR_ERR_OOM, "host memory allocation failed");
+  } catch (const std::exception& ex) {
+    rc = fail(ctx, NR_ERR_INVALID, std::string("internal error: ") + ex.what());
+  }
+  if (rc != NR_OK) {
+    (void)hipStreamSynchronize(ctx->stream);
+    reset_dataset(ctx);
+  }
+  return rc;
 }
 
 int nr_dataset_shape(const nr_ctx* ctx, int64_t* n_nodes, int64_t* n_samples) {
@@ -1067,8 +1034,7 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   if (!src->d_pairs) return fail(dst, NR_ERR_INVALID, "source context has no dataset");
   NR_HIP(dst, hipSetDevice(dst->device));
   NR_HIP(dst, hipStreamSynchronize(dst->stream));
-  dfree(dst->d_pairs);
-  dfree(dst->d_data);
+  reset_dataset(dst);  // on a failure below dst is left with no dataset
   const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2);
   NR_HIP(dst, hipMalloc((void**)&dst->d_pairs, pair_bytes));
   const size_t data_bytes = (size_t)(src->n_samples * (src->n_nodes + 2)) * sizeof(double);  // + virtual columns
@@ -1113,6 +1079,7 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
     return fail(ctx, NR_ERR_INVALID, "module arrays missing");
   NR_HIP(ctx, hipSetDevice(ctx->device));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->modules_gen = -1;  // usable only once everything below has succeeded
   ctx->n_rows = n_rows;
   ctx->n_present = n_present;
   ctx->node_off_h.assign(node_off, node_off + (n_present > 0 ? n_present + 1 : 0));
@@ -1168,6 +1135,7 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->d_data && !ctx->d_disc_nc && n_present > 0)
     return fail(ctx, NR_ERR_INVALID, "dataset has data but disc_contrib is NULL");
+  ctx->modules_gen = ctx->data_gen;
   return NR_OK;
 }
 
@@ -1183,6 +1151,7 @@ int nr_set_null_pool(nr_ctx* ctx, const int32_t* null_idx, int64_t n_null) {
   int rc = upload(ctx, ctx->d_null_idx, null_idx, (size_t)n_null);
   if (rc) return rc;
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->null_gen = ctx->data_gen;
   return NR_OK;
 }
 

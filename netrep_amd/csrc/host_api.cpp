@@ -104,6 +104,21 @@ std::mutex g_hook_mu;
 netrep_interrupt_fn g_hook = nullptr;
 void* g_hook_user = nullptr;
 
+// MonitorProgress's console output replacement (netrep_set_progress_hook).
+netrep_progress_fn g_progress = nullptr;
+void* g_progress_user = nullptr;
+
+void progress_event(int32_t ev, int64_t done, int64_t total) {
+  netrep_progress_fn fn;
+  void* user;
+  {
+    std::lock_guard<std::mutex> lk(g_hook_mu);
+    fn = g_progress;
+    user = g_progress_user;
+  }
+  if (fn) fn(ev, done, total, user);
+}
+
 bool interrupt_requested() {
   netrep_interrupt_fn fn;
   void* user;
@@ -192,6 +207,20 @@ void netrep_set_interrupt_hook(netrep_interrupt_fn fn, void* user) {
   g_hook_user = user;
 }
 
+void netrep_set_progress_hook(netrep_progress_fn fn, void* user) {
+  std::lock_guard<std::mutex> lk(g_hook_mu);
+  g_progress = fn;
+  g_progress_user = user;
+}
+
+int netrep_format_progress(int64_t done, int64_t total, char* buf, int64_t cap) {
+  if (!buf || cap <= 0) return -1;
+  // src/thread-utils.cpp:66-68: round((float)nCompleted / (float)nPerm * 100)
+  const unsigned pct = total > 0 ? (unsigned)std::round((float)done / (float)total * 100.0f) : 0u;
+  const int n = std::snprintf(buf, (size_t)cap, "\r%5u%% completed.", pct);
+  return (n < 0 || n >= cap) ? -1 : n;
+}
+
 void netrep_DiscardPrefetch(void) {
   std::vector<std::unique_ptr<Prefetch>> all;
   {
@@ -202,7 +231,7 @@ void netrep_DiscardPrefetch(void) {
 }
 
 int netrep_PrefetchTestDataset(const double* t_data, const double* t_corr, const double* t_net,
-                               int64_t n_samples, int64_t n_nodes) {
+                               int64_t n_samples, int64_t n_nodes) try {
   if (!t_corr || !t_net || n_nodes <= 0 || (t_data && n_samples < 2))
     return set_err(NR_ERR_INVALID, "invalid arguments to PrefetchTestDataset");
   std::unique_ptr<Prefetch> p(new Prefetch());
@@ -229,6 +258,10 @@ int netrep_PrefetchTestDataset(const double* t_data, const double* t_corr, const
   }
   if (dropped) drop_prefetch(dropped);
   return NR_OK;
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
 }  // extern "C"
@@ -242,7 +275,7 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
                      const char* const* t_names, const char* const* ma_names, const char* const* ma_labels,
                      int64_t n_assign, const char* const* modules, int64_t n_modules, int64_t n_perm,
                      const char* null_hypothesis, int32_t verbose, uint64_t seed, const uint32_t* pi,
-                     double* nulls_out, double* observed_out, CtxPtr preloaded) {
+                     double* nulls_out, double* observed_out, CtxPtr preloaded, int64_t pi_len = -1) {
   if (with_data && !disc->contribution)
     return set_err(NR_ERR_INVALID, "discProps has no 'contribution' but tData was given");
   const std::string null_type = null_hypothesis ? null_hypothesis : "overlap";
@@ -292,6 +325,11 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
   }
   ms.n_present = (int32_t)ms.row_of.size();
   const int n_stat = with_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA;
+  // an explicit shuffle table of a known length must hold n_perm x n_null
+  // entries (the engine reads exactly that many)
+  if (pi && pi_len >= 0 && pi_len != n_perm * (int64_t)ms.null_idx.size())
+    return set_err(NR_ERR_INVALID, "pi holds " + std::to_string(pi_len) + " entries, not nPermutations x n_null = " +
+                                       std::to_string(n_perm) + " x " + std::to_string(ms.null_idx.size()));
 
   int n_dev = 1;
   const int n_gpu = (n_perm > 0) ? (int)std::min<int64_t>(gpu_count_requested(&n_dev), std::max<int64_t>(n_perm, 1)) : 1;
@@ -341,10 +379,7 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
     start[g + 1] = start[g] + n_perm / n_gpu + (g < n_perm % n_gpu ? 1 : 0);
   const int64_t slice = (int64_t)ms.n_rows * n_stat;
   const int64_t n_null = (int64_t)ms.null_idx.size();
-  if (verbose) {
-    std::printf("\n");
-    std::fflush(stdout);
-  }
+  if (verbose) progress_event(NETREP_PROGRESS_BEGIN, 0, n_perm);
   std::atomic<int> running{n_gpu};
   std::vector<std::thread> th;
   for (int g = 0; g < n_gpu; ++g) {
@@ -355,8 +390,9 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
     });
   }
   // Progress monitor (MonitorProgress, src/thread-utils.cpp:49-82): the
-  // calling thread polls progress and the interrupt hook every 100 ms and
-  // prints "% completed." once a second when verbose. On an interrupt every
+  // calling thread polls progress and the interrupt hook every 100 ms and,
+  // when verbose, reports progress through the progress hook once a second
+  // (the library prints nothing itself). On an interrupt every
   // context is cancelled; the workers stop between launches and leave their
   // remaining slices NA, and the partial cube is returned
   // (src/permutations.cpp:375-408) with NR_ERR_CANCELLED.
@@ -371,9 +407,7 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
         nr_progress(ctxs[g].get(), &d, nullptr);
         done += d;
       }
-      const unsigned pct = (unsigned)std::lround((double)done / (double)n_perm * 100.0);
-      std::printf("\r%5u%% completed.", pct);
-      std::fflush(stdout);
+      progress_event(NETREP_PROGRESS_UPDATE, done, n_perm);
       last_print = std::chrono::steady_clock::now();
     }
     if (done_all) break;
@@ -383,10 +417,7 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(100));
   }
-  if (verbose) {
-    std::printf("\n\n");
-    std::fflush(stdout);
-  }
+  if (verbose) progress_event(NETREP_PROGRESS_END, n_perm, n_perm);
   for (auto& t : th) t.join();
   int cancelled_at = -1;
   for (int g = 0; g < n_gpu; ++g) {
@@ -411,8 +442,8 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
                                 int64_t n_assign, const char* const* modules, int64_t n_modules,
                                 int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
                                 int32_t verbose, uint64_t seed, const uint32_t* pi,
-                                double* nulls_out, double* observed_out) {
-  (void)n_cores;
+                                double* nulls_out, double* observed_out) try {
+  nr_set_host_threads(n_cores);  // nThreads bounds the host threads of the call
   if (!disc || !t_corr || !t_net || !t_names || !ma_names || !ma_labels || !modules ||
       !observed_out || n_perm < 0 || (n_perm > 0 && !nulls_out) || n_nodes <= 0)
     return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedure");
@@ -421,6 +452,10 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
   return permutation_impl(disc, t_data != nullptr, t_data, t_corr, t_net, n_samples, n_nodes, t_names, ma_names,
                           ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose, seed, pi,
                           nulls_out, observed_out, std::move(pre));
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
 int netrep_PermutationProcedureFiles(const netrep_disc_props* disc, const char* t_data_file,
@@ -428,9 +463,9 @@ int netrep_PermutationProcedureFiles(const netrep_disc_props* disc, const char* 
                                      const char* const* ma_names, const char* const* ma_labels,
                                      int64_t n_assign, const char* const* modules, int64_t n_modules,
                                      int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
-                                     int32_t verbose, uint64_t seed, const uint32_t* pi,
-                                     double* nulls_out, double* observed_out) {
-  (void)n_cores;
+                                     int32_t verbose, uint64_t seed, const uint32_t* pi, int64_t pi_len,
+                                     double* nulls_out, double* observed_out) try {
+  nr_set_host_threads(n_cores);  // nThreads bounds the host threads of the call
   if (!disc || !t_corr_file || !t_net_file || !ma_names || !ma_labels || !modules || !observed_out ||
       n_perm < 0 || (n_perm > 0 && !nulls_out))
     return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedureFiles");
@@ -451,11 +486,15 @@ int netrep_PermutationProcedureFiles(const netrep_disc_props* disc, const char* 
     return set_err(NR_ERR_INVALID, "the network file has no column names (node names are needed)");
   return permutation_impl(disc, t_data_file != nullptr, nullptr, nullptr, nullptr, n_samples, n_nodes, names.data(),
                           ma_names, ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose,
-                          seed, pi, nulls_out, observed_out, std::move(ctx));
+                          seed, pi, nulls_out, observed_out, std::move(ctx), pi_len);
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
 int netrep_ReadRDSMatrix(const char* path, const char* object, int64_t* nrow, int64_t* ncol, double* out,
-                         char* colnames, int64_t colnames_cap, int64_t* colnames_needed) {
+                         char* colnames, int64_t colnames_cap, int64_t* colnames_needed) try {
   if (!path || !nrow || !ncol) return set_err(NR_ERR_INVALID, "invalid arguments to ReadRDSMatrix");
   nr::RMatrixMeta meta;
   std::vector<double> v;
@@ -474,6 +513,10 @@ int netrep_ReadRDSMatrix(const char* path, const char* object, int64_t* nrow, in
       colnames += s.size() + 1;
     }
   return NR_OK;
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
 int netrep_IntermediateProperties(const double* d_data, const double* d_corr, const double* d_net,
@@ -483,7 +526,7 @@ int netrep_IntermediateProperties(const double* d_data, const double* d_corr, co
                                   int64_t n_assign, const char* const* modules, int64_t n_modules,
                                   double* degree_out, int64_t* degree_len, double* corr_out,
                                   int64_t* corr_len, double* contribution_out,
-                                  int64_t* contribution_len) {
+                                  int64_t* contribution_len) try {
   if (!d_corr || !d_net || !d_names || !t_node_names || !ma_names || !ma_labels || !modules ||
       !degree_out || !degree_len || !corr_out || !corr_len || n_nodes <= 0)
     return set_err(NR_ERR_INVALID, "invalid arguments to IntermediateProperties");
@@ -544,6 +587,10 @@ int netrep_IntermediateProperties(const double* d_data, const double* d_corr, co
     o_n += k;
   }
   return NR_OK;
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
 int netrep_NetProps(const double* data, const double* net, int64_t n_samples, int64_t n_nodes,
@@ -551,7 +598,7 @@ int netrep_NetProps(const double* data, const double* net, int64_t n_samples, in
                     const char* const* ma_labels, int64_t n_assign, const char* const* modules,
                     int64_t n_modules, double* degree_out, double* contribution_out,
                     double* summary_out, double* coherence_out, double* avg_weight_out,
-                    int64_t* k_all_out) {
+                    int64_t* k_all_out) try {
   if (!net || !node_names || !ma_names || !ma_labels || !modules || !degree_out ||
       !avg_weight_out || !k_all_out || n_nodes <= 0)
     return set_err(NR_ERR_INVALID, "invalid arguments to NetProps");
@@ -638,9 +685,13 @@ int netrep_NetProps(const double* data, const double* net, int64_t n_samples, in
     }
   }
   return NR_OK;
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
-int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes, double* scaled_out) {
+int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes, double* scaled_out) try {
   if (!data || !scaled_out || n_samples <= 0 || n_nodes <= 0)
     return set_err(NR_ERR_INVALID, "invalid arguments to Scale");
   CtxPtr ctx;
@@ -649,9 +700,13 @@ int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes, double*
   rc = nr_scale(ctx.get(), data, n_samples, n_nodes, scaled_out);
   if (rc) return ctx_err(rc, ctx.get());
   return NR_OK;
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
-int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol) {
+int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol) try {
   if (!mat || nrow < 0 || ncol < 0) return set_err(NR_ERR_INVALID, "invalid arguments to CheckFinite");
   CtxPtr ctx;
   int rc = open_ctx(0, ctx);
@@ -661,6 +716,10 @@ int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol) {
   if (rc) return ctx_err(rc, ctx.get());
   if (!ok) return set_err(NR_ERR_NONFINITE, "matrices cannot have non-finite or missing values");
   return NR_OK;
+} catch (const std::bad_alloc&) {
+  return set_err(NR_ERR_OOM, "host memory allocation failed");
+} catch (const std::exception& e) {
+  return set_err(NR_ERR_INVALID, std::string("internal error: ") + e.what());
 }
 
 }  // extern "C"

@@ -8,6 +8,7 @@ namespace nr {
 enum { NR_IDX_PRP = 0, NR_IDX_TABLE = 1, NR_IDX_DIRECT = 2 };
 
 constexpr int kProfileWaves = 4;  // waves of the 256-thread profile workgroup (NR_WAVES)
+constexpr int kPackedLayoutK = 320;  // modules of the packed kernel's compile-time LDS layout
 
 // Where the test column of module node c comes from.
 struct IndexSource {
@@ -75,22 +76,15 @@ struct ProfileParams {
   int* queue;                  // work-queue head, zeroed before launch
   int* diag;                   // [0] Lanczos step-cap hits, [1] items, [2] Lanczos steps, [3] reorthogonalisations
   unsigned long long* stamps;  // [8] per-phase shader cycles (diagnostics; NULL = off)
-  int fuse_net;                // 1: each item also computes the network statistics (net)
   int part_global;             // 1: matvec partials (4 x k_max) at the end of the slot's scratch
-  int dual;                    // 1: modules with k > n_samples use the S x S Gram [X' 1]'[X' 1]
   int32_t kvec;                // LDS vector length (0: k_max); larger (dual) modules keep their
                                // per-node arrays in the slot's scratch
   int64_t basis_doubles;       // Lanczos basis doubles per slot (behind the Gram)
   int64_t g32_off;             // doubles from the slot start to the fp32 copy of the packed Gram
                                // (relaxed Lanczos steps; 0: no copy, fp64 matvecs throughout)
-  int32_t start_col;           // 1: Lanczos starts from the packed Gram's column of largest norm
-                               // (its node's row of G), 0: from the near-constant vector
-  int32_t gv_relation;         // 1: G v of the Ritz vector from the Lanczos relation (no extra
-                               // fp64 matvec; primal Gram only), 0: one more matvec
   int32_t order_tail;          // queue order: 0 = module-major (large modules first); T > 0 =
                                // permutation-major over all modules (a size mix in flight) for the
                                // first n_perm - T permutations, the last T module-major
-  NetParams net;
 };
 
 size_t net_kernel_lds(int k_max);
@@ -100,15 +94,10 @@ size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant);
 // Doubles of the packed (chunked column-group) Gram of side kc, rounded to 32.
 int64_t packed_gram_doubles(int kc);
 int profile_kvec_max(int m_max);  // longest LDS vectors of the large-module layout (variant 4)
-int reg_kernel_k_max();  // largest module of the register-resident scheme
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
+// variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);
-// Register-resident 4-wave summary-profile kernel (kernels_rg4.hip).
-size_t rg4_kernel_lds();
-int rg4_kernel_k_max();
-constexpr int kRg4StepCap = 160;  // Lanczos steps (basis columns) per item
-hipError_t launch_profile_rg4(const ProfileParams& P, int n_slots, hipStream_t st);
 hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,
                              hipStream_t st);
 hipError_t launch_symmetry(const double2* a, int64_t n, int* asym, hipStream_t st);

@@ -21,14 +21,6 @@
 #include "kernels.h"
 #include "device_common.h"
 
-// Gram operand pipeline depth (register buffers per wave: 2 = one 16-row step
-// in flight, 3 = two); compile-time A/B via -DNR_GRAM_DEPTH=3. Depth 3 spills
-// in the 3-workgroup kernel (scratch 184 -> 260 B/lane) and measured slower on
-// C3: 72.3 vs 68.8 ms per 1,024-permutation launch (profiles/r02/profile_variants.txt).
-#ifndef NR_GRAM_DEPTH
-#define NR_GRAM_DEPTH 2
-#endif
-
 namespace nr {
 
 
@@ -636,26 +628,8 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
       }
     };
     double cur[4][4];
-#if NR_GRAM_DEPTH >= 3
-    // two steps in flight: three register buffers in rotation; the loads are
-    // unconditional (clamped to the last full step, the surplus unused) so
-    // every wait is a static vmcnt that leaves the later buffers in flight
-    double b1[4][4], b2[4][4];
-    if (full > 0) {
-      ld16(0, cur);
-      ld16(min(16, full - 16), b1);
-    }
-    for (int s0 = 0; s0 < full; s0 += 48) {
-      ld16(min(s0 + 32, full - 16), b2);
-      mfma16(cur);
-      if (s0 + 16 >= full) break;
-      ld16(min(s0 + 48, full - 16), cur);
-      mfma16(b1);
-      if (s0 + 32 >= full) break;
-      ld16(min(s0 + 64, full - 16), b1);
-      mfma16(b2);
-    }
-#else
+    // one 16-row step in flight (a second one spilled in the 3-workgroup
+    // kernel and ran slower: profiles/r02/profile_variants.txt)
     double nxt[4][4];
     if (full > 0) ld16(0, cur);
     for (int s0 = 0; s0 < full; s0 += 16) {
@@ -666,7 +640,6 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
 #pragma unroll
         for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
     }
-#endif
     if (full < S) {  // the last, partial step
 #pragma unroll
       for (int o = 0; o < 4; ++o)
@@ -1361,16 +1334,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   uint32_t* idx_p = L.idx;
   while (next_item<NW>(P, L, s_flags, m, p_local, off, k, kmax,
                        reinterpret_cast<uint32_t*>(gnode + 4 * (int64_t)P.k_max), &idx_p)) {
-    if (P.fuse_net) {
-      // the item's network statistics first (random gathers that overlap the
-      // Gram / Lanczos phases of the co-resident workgroups), in the Lanczos
-      // vectors' LDS, idle until the Gram
-      const NetLds NL = carve_net_over<NW>(L.q, L.red, L.idx, kmax);
-      net_item<NW>(P.net, m, p_local, off, k, NL);
-      if (PACKED)  // its arrays overlap the matvec partials
-        for (int i = tid; i < n_part; i += BS) part[i] = 0.0;
-    }
-    NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
+    NR_STAMP(0);  // queue + index derivation
     LzLds Li = L;  // this item's view: per-node arrays in scratch when k > kmax
     Li.idx = idx_p;
     if (k > kmax) {
@@ -1380,7 +1344,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       Li.w = gnode + 3 * (int64_t)P.k_max;
     }
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
-    const bool dual = P.dual && k > S;
+    const bool dual = k > S;
     const int n = dual ? S : k;  // Lanczos dimension
     const int kc = n + 1;
     double g1[1] = {0.0};
@@ -1402,8 +1366,8 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
         return relax ? packed_matvec<NW, true>(G32, kc, n, x, out, part, kmax, y, L.red)
                      : packed_matvec<NW>(G, kc, n, x, out, part, kmax, y, L.red);
       };
-      const bool q_given = PACKED && P.start_col && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
-      const bool gv_rel = P.gv_relation && !dual;
+      const bool q_given = PACKED && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
+      const bool gv_rel = !dual;
       lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel);
       relax = false;  // node contributions: the fp64 Gram
       if (dual) {
@@ -1426,397 +1390,11 @@ module_profile_kernel(ProfileParams P) {
   profile_body<NR_WAVES, false, 0>(P);
 }
 
-// Packed-Gram variant: 8-wave workgroups, two per CU, so the live Gram
-// working set stays in the Infinity Cache while Lanczos streams it.
-// OCC = waves per SIMD: 4 -> two workgroups per CU (VGPR-capped at 128), 2 -> one.
-template <int KB, int OCC>
-__global__ void __launch_bounds__(512, OCC)
-module_profile_packed_kernel(ProfileParams P) {
-  profile_body<8, true, KB>(P);
-}
-
 // Packed Gram in the lean 4-wave structure (OCC workgroups per CU).
 template <int KB, int OCC>
 __global__ void __launch_bounds__(NR_BS, OCC)
 module_profile_packed4_kernel(ProfileParams P) {
   profile_body<NR_WAVES, true, KB>(P);
-}
-
-// ---------------------------------------------------------------------------
-// Scheme 2 (register-resident, the default for modules of <= 16*RG_TMAX - 1
-// nodes): one 8-wave workgroup per CU. G = [X 1]^T [X 1] is cut into 16 x 16
-// tiles over the upper triangle (T = ceil((k+1)/16) tiles a side, row-major
-// tile ids 0..T(T+1)/2-1); wave w computes the contiguous id range
-// [w*nt/8, (w+1)*nt/8) with v_mfma_f64_16x16x4_f64 and KEEPS the
-// accumulators: its first RG_RT tiles stay in VGPRs, the rest (<= RG_LT) go to
-// an LDS slot in the same lane layout. Those registers are the Lanczos
-// operator: no byte of G ever goes to memory, and a matvec is 8 FMAs per
-// lane per tile plus register butterflies:
-//   type 1 (all tiles):  w_I += G_IJ x_J, lane-local over a run of equal I,
-//                        reduced over the 16 columns by DPP at the run end;
-//   type 2 (I < J):      w_J += G_IJ^T x_I, reduced over the 4 row groups by
-//                        permlane32/16 swaps for 4 tiles at once.
-// Row partials go to per-wave rows (rowp) and column partials to per-tile
-// slots (colp); one pass sums them in a fixed order (deterministic).
-// ---------------------------------------------------------------------------
-constexpr int RG_NW = 8;     // waves per workgroup
-constexpr int RG_RT = 20;    // register tiles per wave (80 doubles of accumulators per lane)
-constexpr int RG_LT = 4;     // LDS tiles per wave
-constexpr int RG_TMAX = 19;  // tiles a side: k + 1 <= 304
-constexpr int RG_KP = 16 * RG_TMAX;
-constexpr int RG_NTMAX = RG_TMAX * (RG_TMAX + 1) / 2;
-static_assert(kProfileWaves == NR_WAVES, "profile workgroup width");
-static_assert((RG_RT + RG_LT) % 4 == 0, "tile groups of four");
-static_assert(RG_NW * (RG_RT + RG_LT) >= RG_NTMAX, "tile capacity");
-static_assert((RG_NTMAX + RG_NW - 1) / RG_NW <= RG_RT + RG_LT, "per-wave tile capacity");
-static_assert(RG_NW * RG_KP + RG_NTMAX * 16 >= RG_KP * 18, "row slab fits the rowp/colp region");
-
-// Rows s .. s+3 of Gram column c: a data column (colofs[c] = idx * S), the
-// virtual all-ones column (-1) or zero padding (-2); rows >= S are zero.
-// Branch-free: every lane loads from a valid address (row clamped, padding
-// columns read column 0) and masks the value afterwards.
-__device__ __forceinline__ void rg_load4(const double* __restrict__ X, int o, int s, int S,
-                                         double (&v)[4]) {
-  const bool data = o >= 0;
-  const double fill = o == -1 ? 1.0 : 0.0;
-  const double* col = X + (data ? o : 0);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int r = s + t;
-    const double x = col[r < S ? r : S - 1];
-    v[t] = r < S ? (data ? x : fill) : 0.0;
-  }
-}
-
-
-// Per-wave tile range of the register scheme: ids [t0, t0 + n); the first
-// nreg = min(n, RG_RT) stay in registers, the remaining nl go to LDS.
-struct RgTiles {
-  int T, nt, t0, n, nreg, nl;  // tiles a side, tiles, this wave's range and split
-  int I0, J0;                  // coordinates of tile t0
-  int Il, Jl;                  // coordinates of tile t0 + nreg (first LDS tile)
-};
-
-// (I, J) of tile id t (t == T(T+1)/2, one past the end, gives (T, T)).
-__device__ __forceinline__ void rg_coords(int T, int t, int& I, int& J) {
-  I = 0;
-  while (I < T && t >= T - I) { t -= T - I; ++I; }
-  J = I + t;
-}
-
-__device__ __forceinline__ RgTiles rg_tiles(int k, int wave) {
-  RgTiles R;
-  R.T = (k + 1 + 15) / 16;
-  R.nt = R.T * (R.T + 1) / 2;
-  R.t0 = wave * R.nt / RG_NW;
-  R.n = (wave + 1) * R.nt / RG_NW - R.t0;
-  R.nreg = R.n < RG_RT ? R.n : RG_RT;
-  R.nl = R.n - R.nreg;
-  rg_coords(R.T, R.t0, R.I0, R.J0);
-  rg_coords(R.T, R.t0 + R.nreg, R.Il, R.Jl);
-  return R;
-}
-
-// Gram tiles acc[t] = G tile (I_t, J_t), t < cnt, the tiles following
-// (I0, J0) in row-major upper-triangle order. The rows go through LDS in
-// slabs of 16: all 512 threads stage rows s0..s0+15 of every column of
-// [X 1] (8 threads x 16 B per column, coalesced; non-finite check here, once
-// per value) into `slab` (column stride RG_SLD doubles: conflict-free
-// ds_read_b128), while the previous slab feeds the MFMAs (register staging,
-// one slab buffer, two barriers per slab). Each lane then feeds rows
-// 4*kk .. 4*kk+3 of its column to 4 MFMAs (the K order permuted identically
-// for both operands); the J block of the next tile is read one tile ahead;
-// a run of equal I starts at its diagonal tile, whose J block is the I block.
-// Every thread of the workgroup must call this (barriers), cnt may be 0.
-constexpr int RG_SLD = 18;
-template <int NTW>
-__device__ __forceinline__ void rg_gram(nr_f64x4 (&acc)[NTW], int T, int I0, int J0, int cnt,
-                                        const double* __restrict__ X, int S, const int* colofs, double* slab,
-                                        int& bad) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int i16 = lane & 15, kk = lane >> 4;
-  const int kp = 16 * T;
-#pragma unroll
-  for (int t = 0; t < NTW; ++t) acc[t] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
-  constexpr int NR = (RG_KP + 63) / 64;  // staging rounds of 64 columns
-  const int part = tid & 7, cbase = tid >> 3;
-  int o[NR];
-#pragma unroll
-  for (int u = 0; u < NR; ++u) {
-    const int c = cbase + 64 * u;
-    o[u] = c < kp ? colofs[c] : -3;  // -3: no such column this item
-  }
-  double st[NR][2];
-  auto stage_load = [&](int s0) {
-    const int r = s0 + 2 * part;
-#pragma unroll
-    for (int u = 0; u < NR; ++u) {
-      const bool data = o[u] >= 0;
-      const double* col = X + (data ? o[u] : 0);
-      const double x0 = col[r < S ? r : S - 1];
-      const double x1 = col[r + 1 < S ? r + 1 : S - 1];
-      const double f = o[u] == -1 ? 1.0 : 0.0;
-      st[u][0] = r < S ? (data ? x0 : f) : 0.0;
-      st[u][1] = r + 1 < S ? (data ? x1 : f) : 0.0;
-      bad |= (int)!isfinite(st[u][0]) | (int)!isfinite(st[u][1]);
-    }
-  };
-  auto blk = [&](int b, double (&v)[4]) {
-    const double* p = slab + (b * 16 + i16) * RG_SLD + 4 * kk;
-    const double2 lo = *reinterpret_cast<const double2*>(p);
-    const double2 hi = *reinterpret_cast<const double2*>(p + 2);
-    v[0] = lo.x;
-    v[1] = lo.y;
-    v[2] = hi.x;
-    v[3] = hi.y;
-  };
-  stage_load(0);
-  for (int s0 = 0; s0 < S; s0 += 16) {
-    __syncthreads();  // the previous slab is consumed
-#pragma unroll
-    for (int u = 0; u < NR; ++u)
-      if (o[u] != -3)
-        *reinterpret_cast<double2*>(slab + (cbase + 64 * u) * RG_SLD + 2 * part) = make_double2(st[u][0], st[u][1]);
-    __syncthreads();
-    if (s0 + 16 < S) stage_load(s0 + 16);  // in flight during the MFMAs below
-    if (cnt > 0) {
-      int I = I0, J = J0;
-      double a[4], b[4], bn[4];
-      if (I0 != J0) blk(I0, a);
-      blk(J0, b);
-#pragma unroll
-      for (int t = 0; t < NTW; ++t) {
-        if (t < cnt) {
-          int In = I, Jn = J + 1;
-          if (Jn == T) {
-            ++In;
-            Jn = In;
-          }
-          if (t + 1 < cnt) blk(Jn, bn);
-          if (J == I) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) a[q] = b[q];
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc[t], 0, 0, 0);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) b[q] = bn[q];
-          I = In;
-          J = Jn;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-}
-
-// Gram epilogue over cnt tiles from (I, J): 1'G1 over the X block (weight 2
-// off the diagonal), the diagonal, the column means (column k holds the
-// column sums), and -- for LDS tiles -- the store into the wave's slot.
-template <int NTW>
-__device__ __forceinline__ void rg_epilogue(const nr_f64x4 (&acc)[NTW], int T, int I, int J, int cnt, int k,
-                                            double Sd, double& g1, double* gdiag, double* colm, double* lt) {
-  const int lane = threadIdx.x & 63;
-  const int i16 = lane & 15, kk = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < NTW; ++t) {
-    if (t < cnt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = I * 16 + kk + 4 * r, gj = J * 16 + i16;
-        const double v = acc[t][r];
-        if (gi < k && gj < k) g1 += (I == J ? 1.0 : 2.0) * v;
-        if (gi == gj) gdiag[gi] = v;
-        if (gj == k) colm[gi] = v / Sd;  // column sums -> means (rows gi <= k)
-        if (lt) lt[t * 256 + r * 64 + lane] = v;
-      }
-      if (++J == T) {
-        ++I;
-        J = I;
-      }
-    }
-  }
-}
-
-template <int NTW>
-struct RgMatvec {
-  nr_f64x4 (&acc)[RG_RT];
-  const RgTiles& R;
-  const double* ltile;  // this wave's LDS tiles [RG_LT][4][64]
-  double* rowp;         // [RG_NW][RG_KP]
-  double* colp;         // [RG_NTMAX][16]
-  double* red;
-  int k;
-
-  // out = G x for rows < k; returns y . out (block-wide) when y != NULL.
-  // x must be zero from k to 16*T.
-  __device__ __forceinline__ double operator()(const double* x, double* out, const double* y) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int i16 = lane & 15, kk = lane >> 4;
-    const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
-    const int rrow = kk + 4 * (2 * ((lane >> 3) & 1) + ((lane >> 2) & 1));
-    // Opaque per call: otherwise the per-tile address arithmetic is hoisted
-    // out of the Lanczos loop and pins dozens of VGPRs next to the tiles.
-    int I = R.I0, J = R.J0, n = R.n, t0 = R.t0, T = R.T;
-    asm volatile("" : "+s"(I), "+s"(J), "+s"(n), "+s"(t0), "+s"(T));
-    double ra[4] = {0.0, 0.0, 0.0, 0.0};
-    double xi[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) xi[r] = x[I * 16 + kk + 4 * r];
-    double cx[4];
-    int cid[4];
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      if (t < n) {
-        double g[4];
-        if (t < RG_RT) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) g[r] = acc[t][r];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) g[r] = ltile[(t - RG_RT) * 256 + r * 64 + lane];
-        }
-        const double xj = x[J * 16 + i16];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ra[r] = fma(g[r], xj, ra[r]);
-        if (I != J) {
-          double c = 0.0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) c = fma(g[r], xi[r], c);
-          cx[t & 3] = c;
-          cid[t & 3] = t0 + t;
-        } else {
-          cx[t & 3] = 0.0;
-          cid[t & 3] = -1;
-        }
-        if (++J == T || t + 1 == n) {  // end of a run of equal I
-          const double v = rg_row_reduce(ra, lane);
-          if ((lane & 3) == 0) rowp[wave * RG_KP + I * 16 + rrow] = v;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ra[r] = 0.0;
-          if (J == T) {
-            ++I;
-            J = I;
-            if (t + 1 < n) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) xi[r] = x[I * 16 + kk + 4 * r];
-            }
-          }
-        }
-      } else {
-        cx[t & 3] = 0.0;
-        cid[t & 3] = -1;
-      }
-      if ((t & 3) == 3 && t - 3 < n) {
-        const double a0 = nr_swap32_sum(cx[0], cx[1]);
-        const double a1 = nr_swap32_sum(cx[2], cx[3]);
-        const double v = nr_swap16_sum(a0, a1);
-        const int sl = 2 * b4 + b5;
-        const int id = sl == 0 ? cid[0] : sl == 1 ? cid[1] : sl == 2 ? cid[2] : cid[3];
-        if (id >= 0) colp[id * 16 + i16] = v;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-    // out_r = sum_w rowp[w][r] + sum_{I < J(r)} colp[id(I, J(r))][r mod 16];
-    // rowp is zeroed as it is consumed (only runs write it).
-    double d[1] = {0.0};
-    const int kp = 16 * R.T;
-    for (int rr = threadIdx.x; rr < kp; rr += RG_NW * 64) {
-      double s = 0.0;
-#pragma unroll
-      for (int w = 0; w < RG_NW; ++w) {
-        s += rowp[w * RG_KP + rr];
-        rowp[w * RG_KP + rr] = 0.0;
-      }
-      const int Jr = rr >> 4, c = rr & 15;
-      int id = Jr;  // id(0, Jr)
-      for (int Ii = 0; Ii < Jr; ++Ii) {
-        s += colp[id * 16 + c];
-        id += R.T - Ii - 1;
-      }
-      if (rr < k) {
-        out[rr] = s;
-        if (y) d[0] += y[rr] * s;
-      }
-    }
-    block_sums<1, RG_NW>(d, red);
-    return d[0];
-  }
-};
-
-size_t reg_kernel_lds(int m_max);
-
-__global__ void __launch_bounds__(RG_NW * 64, 2)
-module_profile_reg_kernel(ProfileParams P) {
-  constexpr int NW = RG_NW, BS = NW * 64, NTW = RG_RT + RG_LT;
-  uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int s_flags[8];
-  const int mmax = RG_KP < 160 ? RG_KP : 160;
-  const int S = (int)P.n_samples;
-  double* ex;
-  const int64_t extra = (int64_t)NW * RG_KP + (int64_t)RG_NTMAX * 16 + RG_KP + (int64_t)NW * RG_LT * 256 +
-                        RG_KP / 2;
-  const LzLds L = carve_lds<NW>(smem, RG_KP, mmax, extra, &ex);
-  double* rowp = ex;                              // [NW][KP]
-  double* colp = rowp + NW * RG_KP;               // [NTMAX][16]
-  double* gdiag = colp + RG_NTMAX * 16;           // [KP]
-  double* ltiles = gdiag + RG_KP;                 // [NW][LT][256]
-  int* colofs = reinterpret_cast<int*>(ltiles + NW * RG_LT * 256);  // [KP]
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  double* Q = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;  // Lanczos basis
-  const double* __restrict__ X = P.data;
-  const double Sd = (double)S;
-  double* ltile = ltiles + wave * RG_LT * 256;
-  for (int i = tid; i < NW * RG_KP; i += BS) rowp[i] = 0.0;
-
-  int m, k;
-  int64_t p_local, off;
-  while (next_item<NW>(P, L, s_flags, m, p_local, off, k)) {
-    NR_STAMP(0);  // queue + index derivation (+ fused network statistics)
-    const RgTiles R = rg_tiles(k, wave);
-    const int kp = 16 * R.T;
-    for (int c = tid; c < kp; c += BS) {
-      colofs[c] = c < k ? (int)L.idx[c] * S : (c == k ? -1 : -2);
-      if (c >= k) {  // the Lanczos inputs are zero beyond k
-        L.q[c] = 0.0;
-        L.vv[c] = 0.0;
-      }
-    }
-    __syncthreads();
-    NR_STAMP(6);  // tile ranges, column offsets
-    // ---- Gram tiles on the matrix cores, kept where they were computed ----
-    int bad = 0;
-    double g1[1] = {0.0};
-    // The row slabs are staged in the rowp/colp region (idle until the
-    // Lanczos matvecs); pass 1 only where some wave overflows into LDS.
-    double* slab = rowp;
-    if ((R.nt + NW - 1) / NW > RG_RT) {  // pass 1: the tiles that overflow into the LDS slots
-      nr_f64x4 accl[RG_LT];
-      rg_gram<RG_LT>(accl, R.T, R.Il, R.Jl, R.nl, X, S, colofs, slab, bad);
-      rg_epilogue<RG_LT>(accl, R.T, R.Il, R.Jl, R.nl, k, Sd, g1[0], gdiag, L.colm, ltile);
-    }
-    nr_f64x4 acc[RG_RT];  // pass 2: the register tiles (live until the item ends)
-    rg_gram<RG_RT>(acc, R.T, R.I0, R.J0, R.nreg, X, S, colofs, slab, bad);
-    rg_epilogue<RG_RT>(acc, R.T, R.I0, R.J0, R.nreg, k, Sd, g1[0], gdiag, L.colm, nullptr);
-    if (bad) atomicOr(&s_flags[1], 1);
-    __syncthreads();  // slab reads done before rowp is cleared
-    for (int i = tid; i < NW * RG_KP; i += BS) rowp[i] = 0.0;
-    block_sums<1, NW>(g1, L.red);  // barriers also publish gdiag, colm and the LDS tiles
-    NR_STAMP(1);  // Gram
-    if (s_flags[1] == 0) {
-      RgMatvec<NTW> mv{acc, R, ltile, rowp, colp, L.red, k};
-      lanczos_ritz<NW, false>(P, k, L, s_flags, Q, mv, t_mark);
-      profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) { return gdiag[c]; });
-    } else {
-      profile_nonfinite<NW>(P, k, m, S, L);
-    }
-    profile_stats<NW>(P, k, m, off, p_local, L);
-    NR_STAMP(5);  // Ritz vector, contributions, statistics
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1939,19 +1517,10 @@ size_t net_kernel_lds(int k_max) {
 size_t net_big_slot_bytes(int k_max) { return (net_lds_bytes(4, k_max) + 255) / 256 * 256; }
 
 // Compile-time module-size bucket of the packed kernel (0 = runtime layout).
-int packed_bucket(int k_max) { return k_max <= 320 ? 320 : 0; }
+int packed_bucket(int k_max) { return k_max <= kPackedLayoutK ? kPackedLayoutK : 0; }
 
-size_t reg_kernel_lds(int m_max) {
-  (void)m_max;  // compile-time layout (mmax = 160)
-  const size_t mmax = RG_KP < 160 ? RG_KP : 160;
-  const size_t extra = (size_t)RG_NW * RG_KP + (size_t)RG_NTMAX * 16 + RG_KP + (size_t)RG_NW * RG_LT * 256 + RG_KP / 2;
-  return sizeof(double) * (8 * RG_NW + 6 * (size_t)RG_KP + extra + 12 * mmax + 3) + sizeof(uint32_t) * RG_KP;
-}
-
-int reg_kernel_k_max() { return RG_KP - 1; }
-
-// variant: 0 full Gram (4 waves), 1 packed (8 waves), 2 packed (4 waves),
-// 3 register-resident (8 waves, one workgroup per CU)
+// variant: 0 full Gram, 2 packed Gram, 4 full Gram with the matvec partials
+// in global scratch (all 4-wave workgroups)
 int profile_kvec_max(int m_max) {
   const size_t fixed = sizeof(double) * (8 * NR_WAVES + 12 * (size_t)m_max + 3);
   const size_t per = 6 * sizeof(double) + sizeof(uint32_t);
@@ -1960,11 +1529,10 @@ int profile_kvec_max(int m_max) {
 
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
   (void)n_samples;
-  if (variant == 3) return reg_kernel_lds(m_max);
   if (variant == 4)  // full Gram, matvec partials in global scratch
     return sizeof(double) * (8 * NR_WAVES + 6 * (size_t)k_max + 12 * (size_t)m_max + 3) + sizeof(uint32_t) * k_max;
   const bool packed = variant != 0;
-  const int nw = variant == 1 ? 8 : NR_WAVES;
+  const int nw = NR_WAVES;
   if (packed && packed_bucket(k_max) > 0) {
     k_max = packed_bucket(k_max);
     m_max = k_max < 160 ? k_max : 160;
@@ -1996,34 +1564,18 @@ hipError_t launch_net(const NetParams& P0, int64_t n_items, hipStream_t st) {
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st) {
   const size_t lds = profile_kernel_lds(P.kvec > 0 ? P.kvec : P.k_max, P.m_max, (int)P.n_samples, variant);
-  const dim3 g((unsigned)n_slots), b(512), b4(NR_BS);
-  const bool b320 = packed_bucket(P.k_max) == 320;
-  const bool packed = variant == 1;
-  if (variant == 3) {
-    hipLaunchKernelGGL(module_profile_reg_kernel, g, dim3(RG_NW * 64), lds, st, P);
-    return hipGetLastError();
-  }
+  const dim3 g((unsigned)n_slots), b4(NR_BS);
   if (variant == 2) {
-    if (b320 && wg_per_cu >= 4)
-      hipLaunchKernelGGL((module_profile_packed4_kernel<320, 4>), g, b4, lds, st, P);
-    else if (b320 && wg_per_cu >= 3)
-      hipLaunchKernelGGL((module_profile_packed4_kernel<320, 3>), g, b4, lds, st, P);
-    else if (b320)
-      hipLaunchKernelGGL((module_profile_packed4_kernel<320, 2>), g, b4, lds, st, P);
+    // the compile-time layout of modules of <= 320 nodes at three workgroups
+    // per CU (measured fastest: profiles/r02/profile_variants.txt), else the
+    // runtime layout
+    if (packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
+      hipLaunchKernelGGL((module_profile_packed4_kernel<kPackedLayoutK, 3>), g, b4, lds, st, P);
     else
       hipLaunchKernelGGL((module_profile_packed4_kernel<0, 2>), g, b4, lds, st, P);
     return hipGetLastError();
   }
-  if (packed && b320 && wg_per_cu >= 2)
-    hipLaunchKernelGGL((module_profile_packed_kernel<320, 4>), g, b, lds, st, P);
-  else if (packed && b320)
-    hipLaunchKernelGGL((module_profile_packed_kernel<320, 2>), g, b, lds, st, P);
-  else if (packed && wg_per_cu >= 2)
-    hipLaunchKernelGGL((module_profile_packed_kernel<0, 4>), g, b, lds, st, P);
-  else if (packed)
-    hipLaunchKernelGGL((module_profile_packed_kernel<0, 2>), g, b, lds, st, P);
-  else
-    hipLaunchKernelGGL(module_profile_kernel, dim3((unsigned)n_slots), dim3(NR_BS), lds, st, P);
+  hipLaunchKernelGGL(module_profile_kernel, g, b4, lds, st, P);
   return hipGetLastError();
 }
 

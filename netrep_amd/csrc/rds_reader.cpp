@@ -19,7 +19,7 @@ namespace {
 
 enum : int {
   kSym = 1, kList = 2, kClos = 3, kProm = 5, kLang = 6, kChar = 9, kLgl = 10, kInt = 13, kReal = 14,
-  kCplx = 15, kStr = 16, kDot = 17, kVec = 19, kExpr = 20, kRaw = 24, kS4 = 25,
+  kCplx = 15, kStr = 16, kDot = 17, kVec = 19, kExpr = 20, kRaw = 24, kS4 = 25, kAltrep = 238,
   kBaseEnv = 241, kEmptyEnv = 242, kMissingArg = 251, kUnbound = 252, kGlobalEnv = 253,
   kNil = 254, kRef = 255
 };
@@ -74,6 +74,8 @@ bool RMatrixReader::length_field(int64_t* n) {
   int32_t hi, lo;
   if (!i32(&hi) || !i32(&lo)) return false;
   *n = ((int64_t)(uint32_t)hi << 32) | (int64_t)(uint32_t)lo;
+  // R_XLEN_T_MAX = 2^52: a larger long length is a corrupt or forged header
+  if (*n < 0 || *n > ((int64_t)1 << 52)) return fail("vector length beyond R's limit (corrupt file)");
   return true;
 }
 
@@ -114,8 +116,16 @@ bool RMatrixReader::read_charsxp(std::string* s, bool* na) {
   s->clear();
   if (n == -1) return true;
   if (n < 0) return fail("bad string length");
-  s->resize((size_t)n);
-  return n == 0 || bytes(&(*s)[0], n);
+  // grown as the bytes arrive: a forged length ends at the end of the stream,
+  // not in a multi-gigabyte allocation
+  char buf[4096];
+  for (int32_t left = n; left > 0;) {
+    const int32_t part = left < (int32_t)sizeof(buf) ? left : (int32_t)sizeof(buf);
+    if (!bytes(buf, part)) return false;
+    s->append(buf, (size_t)part);
+    left -= part;
+  }
+  return true;
 }
 
 // A tag: a symbol (recorded for later back-references) or a back-reference.
@@ -172,7 +182,7 @@ bool RMatrixReader::skip_item(int depth) {
       int64_t n;
       if (!length_field(&n)) return false;
       const int64_t w = type == kReal ? 8 : type == kCplx ? 16 : type == kRaw ? 1 : 4;
-      if (!skip(n * w)) return false;
+      if (!skip(n * w)) return false;  // n <= 2^52 (length_field): no overflow
       return !has_attr || skip_item(depth + 1);
     }
     case kStr: case kVec: case kExpr: {
@@ -184,6 +194,12 @@ bool RMatrixReader::skip_item(int depth) {
     }
     case kS4:
       return !has_attr || skip_item(depth + 1);
+    case kAltrep:
+      // R >= 3.5 compact / deferred vectors (e.g. dimnames from
+      // as.character(1:n)) are not decoded: re-save with
+      // saveRDS(unserialize(serialize(x, NULL, version = 2)))
+      return fail("ALTREP-encoded object (R >= 3.5 compact vector) is not supported; re-save the matrix "
+                  "with serialisation version 2");
     default:
       return fail("unsupported item type " + std::to_string(type) + " in the serialised stream");
   }
@@ -255,14 +271,18 @@ bool RMatrixReader::read_string_vector(std::vector<std::string>* out, int depth)
   const int type = flags & 0xFF;
   out->clear();
   if (type == kNil) return true;
+  if (type == kAltrep)
+    return fail("ALTREP-encoded dimnames (R >= 3.5 compact vector) are not supported; re-save the matrix "
+                "with serialisation version 2");
   if (type != kStr) return fail("dimnames entry is not a character vector");
   int64_t n;
   if (!length_field(&n)) return false;
-  out->resize((size_t)n);
+  out->reserve((size_t)(n < (1 << 16) ? n : (1 << 16)));  // grown as the strings arrive
   for (int64_t i = 0; i < n; ++i) {
     bool na;
-    if (!read_charsxp(&(*out)[(size_t)i], &na)) return false;
-    if (na) (*out)[(size_t)i] = "NA";
+    std::string s;
+    if (!read_charsxp(&s, &na)) return false;
+    out->push_back(na ? std::string("NA") : std::move(s));
   }
   return !(flags & (1 << 9)) || skip_item(depth + 1);
 }
@@ -310,7 +330,7 @@ bool RMatrixReader::finish(RMatrixMeta* meta) {
   if (consumed_ != length_) return fail("matrix payload not fully read");
   *meta = RMatrixMeta();
   if (has_attr_ && !read_attributes(meta, 1)) return false;
-  if (meta->nrow <= 0 && meta->ncol <= 0) return fail("the object has no dim attribute (not a matrix)");
+  if (meta->nrow <= 0 || meta->ncol <= 0) return fail("the object has no (positive) dim attribute (not a matrix)");
   if (meta->nrow * meta->ncol != length_) return fail("dim does not match the payload length");
   if (!meta->rownames.empty() && (int64_t)meta->rownames.size() != meta->nrow) return fail("bad rownames length");
   if (!meta->colnames.empty() && (int64_t)meta->colnames.size() != meta->ncol) return fail("bad colnames length");
@@ -324,7 +344,12 @@ bool read_matrix_host(const char* path, const char* name, RMatrixMeta* meta, std
   if (ok) {
     const int64_t n = r.length();
     if (want_values) {
-      values->resize((size_t)n);
+      try {
+        values->resize((size_t)n);
+      } catch (const std::exception&) {
+        if (err) *err = "cannot allocate " + std::to_string(n) + " doubles for the matrix";
+        return false;
+      }
       ok = r.read_raw(values->data(), n);
       if (ok) {
         unsigned char* p = reinterpret_cast<unsigned char*>(values->data());

@@ -122,6 +122,12 @@ class Engine:
         self.n_nodes = other.n_nodes
         self.n_samples = other.n_samples
 
+    def shape(self):
+        """(n_nodes, n_samples) of the resident dataset; (0, 0) when there is none."""
+        n, s_ = C.c_int64(), C.c_int64()
+        self._check(self._lib.nr_dataset_shape(self._h, C.byref(n), C.byref(s_)))
+        return n.value, s_.value
+
     def symmetric(self) -> bool:
         v = C.c_int()
         self._check(self._lib.nr_dataset_symmetric(self._h, C.byref(v)))

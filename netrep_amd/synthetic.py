@@ -23,6 +23,8 @@ CONFIGS = {
     "C3": (20000, 500, np.round(np.linspace(30, 300, 50)).astype(int), 100_000, True),
     "C4": (20000, 500, np.round(np.linspace(30, 300, 50)).astype(int), 1_000_000, False),
     "C5": (40000, 1000, np.round(np.geomspace(30, 2000, 40)).astype(int), 100, True),
+    # small case of the same shape for the multi-rank GPU test (tests/test_gpu_distributed.py)
+    "CT": (3000, 120, np.round(np.linspace(30, 300, 8)).astype(int), 192, True),
 }
 
 

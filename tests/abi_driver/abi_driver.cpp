@@ -9,6 +9,10 @@
 //   abi_driver interrupt <dir>  same case, with an interrupt hook that fires
 //                               on its 3rd poll (~200 ms in); writes the
 //                               partial cube and rc
+//   abi_driver progress <dir>   same case with verbose = 1 and a progress
+//                               hook that records every call (progress.txt:
+//                               "event done total" lines) -- the library
+//                               itself must print nothing
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -56,11 +60,22 @@ std::vector<const char*> cstrs(const std::vector<std::string>& v) {
 std::atomic<int> g_polls{0};
 int interrupt_on_third_poll(void*) { return ++g_polls >= 3 ? 1 : 0; }
 
+// The Rcpp glue would write netrep_format_progress's line to Rcpp::Rcout
+// (INTEGRATION.md); here every call is recorded with the formatted line.
+void record_progress(int32_t event, int64_t done, int64_t total, void* user) {
+  auto* log = static_cast<std::vector<std::string>*>(user);
+  char line[64] = "";
+  if (event == NETREP_PROGRESS_UPDATE) netrep_format_progress(done, total, line, sizeof(line));
+  std::ostringstream s;
+  s << event << " " << done << " " << total << " " << (line[0] ? line + 1 : "-");  // drop the '\r'
+  log->push_back(s.str());
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    std::fprintf(stderr, "usage: abi_driver perm|interrupt <dir>\n");
+    std::fprintf(stderr, "usage: abi_driver perm|interrupt|progress <dir>\n");
     return 2;
   }
   const std::string mode = argv[1], dir = std::string(argv[2]) + "/";
@@ -109,11 +124,18 @@ int main(int argc, char** argv) {
   const int n_stat = with_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA;
   std::vector<double> nulls((size_t)(M * n_stat * n_perm)), observed(M * n_stat);
   if (mode == "interrupt") netrep_set_interrupt_hook(interrupt_on_third_poll, nullptr);
+  std::vector<std::string> progress_log;
+  if (mode == "progress") netrep_set_progress_hook(record_progress, &progress_log);
   const int rc = netrep_PermutationProcedure(
       &dp, with_data ? data.data() : nullptr, corr.data(), net.data(), S, N, tn.data(), an.data(), al.data(),
-      (int64_t)an.size(), mn.data(), (int64_t)M, n_perm, 1, null_h.c_str(), 0, seed,
+      (int64_t)an.size(), mn.data(), (int64_t)M, n_perm, 1, null_h.c_str(), mode == "progress" ? 1 : 0, seed,
       use_pi ? pi.data() : nullptr, nulls.data(), observed.data());
   netrep_set_interrupt_hook(nullptr, nullptr);
+  netrep_set_progress_hook(nullptr, nullptr);
+  if (mode == "progress") {
+    std::ofstream pf(dir + "progress.txt");
+    for (const auto& s : progress_log) pf << s << "\n";
+  }
   std::ofstream(dir + "rc.txt") << rc << "\n" << netrep_last_error() << "\n";
   write_bin(dir + "nulls.f64", nulls.data(), nulls.size());
   write_bin(dir + "observed.f64", observed.data(), observed.size());

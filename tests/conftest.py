@@ -62,3 +62,40 @@ def assert_stats_close(got, exp, rtol=RTOL, floor=FLOOR, what=""):
         assert err.max() <= rtol, (f"{what}: max scaled error {err.max():.3e} at index {at}: "
                                    f"got {got[at]!r}, expected {exp[at]!r}")
     return float(err.max()) if err.size else 0.0
+
+
+# The north star's "p-values must be identical" (R/pperm.R:138-151): the
+# reference's p-values come from exact counts #(null <= obs) and #(null >= obs)
+# after dropping NA, then permp. The GPU cube with its observed statistics and
+# the oracle cube with its own must give the same counts and -- through the
+# same host p-value code -- bitwise the same p-values for every (module,
+# statistic) and every alternative. Returns a record: count mismatches
+# (expected 0) and the closest approach of a null value to its observed value
+# (scaled as assert_stats_close scales errors), i.e. the margin a near-tie
+# would need to flip a count.
+def assert_pvalues_identical(nulls_g, obs_g, nulls_o, obs_o, n_vars, total_size, what=""):
+    from netrep_amd.pvalues import extreme_counts, permutationTest
+    nulls_g, nulls_o = np.asarray(nulls_g, np.float64), np.asarray(nulls_o, np.float64)
+    obs_g, obs_o = np.asarray(obs_g, np.float64), np.asarray(obs_o, np.float64)
+    lg, mg, ng = extreme_counts(nulls_g, obs_g)
+    lo, mo, no = extreme_counts(nulls_o, obs_o)
+    bad = (lg != lo) | (mg != mo) | (ng != no)
+    fin = np.isfinite(nulls_o) & np.isfinite(obs_o)[:, :, None]
+    gap = np.abs(nulls_o - obs_o[:, :, None]) / np.maximum(np.abs(obs_o[:, :, None]), FLOOR)
+    gap = np.where(fin, gap, np.inf)
+    exact_ties = int(np.sum(gap == 0.0))
+    nonzero = gap[(gap > 0.0) & np.isfinite(gap)]
+    closest = float(nonzero.min()) if nonzero.size else float("inf")
+    if bad.any():
+        at = [tuple(int(v) for v in i) for i in np.argwhere(bad)[:5]]
+        raise AssertionError(f"{what}: extreme counts differ at (module, statistic) {at}; "
+                             f"closest |null - obs| there {[float(gap[i].min()) for i in at]}")
+    n_stat = obs_o.shape[1]
+    statnames = None if n_stat in (4, 7) else [str(i) for i in range(n_stat)]
+    for alt in ("greater", "less", "two.sided"):
+        pg = permutationTest(nulls_g, obs_g, n_vars, total_size, alt, statnames)
+        po = permutationTest(nulls_o, obs_o, n_vars, total_size, alt, statnames)
+        same = (pg.view(np.uint64) == po.view(np.uint64)) | (np.isnan(pg) & np.isnan(po))
+        assert same.all(), f"{what}: {alt} p-values differ at {np.argwhere(~same)[:5].tolist()}"
+    return {"count_mismatches": int(bad.sum()), "exact_ties": exact_ties,
+            "closest_nonzero_scaled_gap": closest, "cells": int(bad.size)}

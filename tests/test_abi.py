@@ -46,3 +46,18 @@ def test_no_cpu_fallback_without_gpu():
     assert "no CPU fallback" in str(ei.value)
     with pytest.raises(netrep_amd.NetRepError):
         netrep_amd.Scale(np.ones((3, 2)))
+
+
+def test_format_progress_matches_reference_line():
+    """netrep_format_progress renders MonitorProgress's "\\r%5d% completed."
+    with round((float)done / (float)total * 100) (src/thread-utils.cpp:66-68)."""
+    from netrep_amd.api import format_progress
+    assert format_progress(0, 10000) == "\r    0% completed."
+    assert format_progress(5000, 10000) == "\r   50% completed."
+    assert format_progress(10000, 10000) == "\r  100% completed."
+    assert format_progress(1, 3) == "\r   33% completed."
+    assert format_progress(2, 3) == "\r   67% completed."
+    import ctypes as C
+    import netrep_amd._lib as L
+    buf = C.create_string_buffer(8)
+    assert L.load().netrep_format_progress(1, 2, buf, 8) == -1   # too small: refused, not truncated

@@ -203,3 +203,30 @@ def test_shared_device_two_contexts_bitwise_equal(monkeypatch):
     monkeypatch.setenv("NETREP_NUM_GPUS", "3")
     three = N.PermutationProcedure(*args, seed=11)
     np.testing.assert_array_equal(one["nulls"].view(np.uint64), three["nulls"].view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_progress_hook_replaces_console_output(tmp_path):
+    """verbose = 1 with netrep_set_progress_hook (VERDICT r2 item 3,
+    MonitorProgress src/thread-utils.cpp:54-81): the hook sees BEGIN, UPDATEs
+    with non-decreasing counts formatted as the reference's "%5d% completed."
+    line and a final done == total update, then END -- and the library writes
+    nothing to stdout / stderr itself."""
+    case = _long_case()
+    n_perm = 150_000
+    d = str(tmp_path / "prog")
+    write_case(d, **case, n_perm=n_perm, seed=5, null="overlap")
+    r = subprocess.run([DRIVER, "progress", d], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == "" and r.stderr == "", (r.stdout[:200], r.stderr[:200])
+    rc = int(open(os.path.join(d, "rc.txt")).read().split("\n")[0])
+    assert rc == 0
+    lines = [ln.split(" ", 3) for ln in open(os.path.join(d, "progress.txt")).read().splitlines()]
+    events = [int(x[0]) for x in lines]
+    assert events[0] == 0 and events[-1] == 2 and set(events[1:-1]) == {1}, events
+    upd = [(int(x[1]), int(x[2]), x[3]) for x in lines if x[0] == "1"]
+    assert len(upd) >= 2
+    done = [u[0] for u in upd]
+    assert done == sorted(done) and done[-1] == n_perm and all(u[1] == n_perm for u in upd)
+    for dn, tot, text in upd:
+        assert text == "%5d%% completed." % round(np.float32(dn) / np.float32(tot) * 100)

@@ -33,7 +33,7 @@ from netrep_amd.api import RMatrix
 from oracle import netrep_oracle as O
 from oracle import ref_cpp
 
-from conftest import ROOT, assert_stats_close
+from conftest import ROOT, assert_pvalues_identical, assert_stats_close
 
 pytestmark = pytest.mark.gpu
 
@@ -59,6 +59,11 @@ def _report():
 def record(name, err, **extra):
     REPORT[name] = dict(max_scaled_error=err, **extra)
     print(f"{name}: max scaled error {err:.3e} {extra}")
+
+
+def record_pvalues(name, rec):
+    REPORT["p-values: " + name] = rec
+    print(f"p-values {name}: {rec}")
 
 
 def _torch():
@@ -158,21 +163,13 @@ def test_c3_nulls_vs_cpp_oracle(c3):
     seed, p0 = 0x5EED, 123_456
     got = c3.eng.run(p0, p0 + 64, seed)
     exp, obs = c3.oracle(p0, p0 + 64, seed, True)
-    e1 = assert_stats_close(c3.eng.observed(), obs, what="C3 observed")
+    gobs = c3.eng.observed()
+    e1 = assert_stats_close(gobs, obs, what="C3 observed")
     e2 = assert_stats_close(got, exp, what="C3 nulls")
     record("C3 nulls (64 perms x 50 modules, S=500)", max(e1, e2), perms=64)
-
-
-def test_c3_nulls_fused_network_phase(c3, monkeypatch):
-    """The opt-in fused kernel (NETREP_FUSE=1: network statistics inside the
-    summary-profile item loop) gives the same nulls as the separate launches."""
-    seed, p0 = 0x5EED, 5_000
-    base = c3.eng.run(p0, p0 + 32, seed)
-    monkeypatch.setenv("NETREP_FUSE", "1")
-    got = c3.eng.run(p0, p0 + 32, seed)
-    assert_stats_close(got, base, what="C3 fused vs separate")
-    exp, _ = c3.oracle(p0, p0 + 32, seed, True)
-    record("C3 nulls, fused network phase (32 perms)", assert_stats_close(got, exp, what="C3 fused"), perms=32)
+    k = np.diff(c3.node_off)
+    record_pvalues("C3 (64 perms x 50 modules x 7 statistics)",
+                   assert_pvalues_identical(got, gobs, exp, obs, k, c3.n, what="C3"))
 
 
 def test_c4_network_only_full_size(c3):
@@ -180,9 +177,12 @@ def test_c4_network_only_full_size(c3):
     seed, p0 = 77, 9_000
     got = c3.eng_nodata.run(p0, p0 + 256, seed)
     exp, obs = c3.oracle(p0, p0 + 256, seed, False)
-    e1 = assert_stats_close(c3.eng_nodata.observed(), obs, what="C4 observed")
+    gobs = c3.eng_nodata.observed()
+    e1 = assert_stats_close(gobs, obs, what="C4 observed")
     e2 = assert_stats_close(got, exp, what="C4 nulls")
     record("C4 nulls (256 perms x 50 modules, network only)", max(e1, e2), perms=256)
+    record_pvalues("C4 (256 perms x 50 modules x 4 statistics)",
+                   assert_pvalues_identical(got, gobs, exp, obs, np.diff(c3.node_off), c3.n, what="C4"))
 
 
 def test_c2_exact_shape():
@@ -192,9 +192,12 @@ def test_c2_exact_shape():
         seed, p0 = 42, 0
         got = c.eng.run(p0, p0 + 256, seed)
         exp, obs = c.oracle(p0, p0 + 256, seed, True)
-        e1 = assert_stats_close(c.eng.observed(), obs, what="C2 observed")
+        gobs = c.eng.observed()
+        e1 = assert_stats_close(gobs, obs, what="C2 observed")
         e2 = assert_stats_close(got, exp, what="C2 nulls")
         record("C2 nulls (256 perms x 20 modules, S=100)", max(e1, e2), perms=256)
+        record_pvalues("C2 (256 perms x 20 modules x 7 statistics)",
+                       assert_pvalues_identical(got, gobs, exp, obs, np.diff(c.node_off), c.n, what="C2"))
     finally:
         c.close()
 
@@ -243,6 +246,7 @@ def test_c5_three_datasets_null_all():
         o += k
         ocv += k * (k - 1) // 2
     errs = []
+    pv = []
     for t in range(3):
         # test dataset t: all 40,000 genes in a dataset-specific column order;
         # its modules are the discovery modules (mapped through the names)
@@ -277,6 +281,15 @@ def test_c5_three_datasets_null_all():
             np.concatenate([disc["contribution"][m] for m in mods]), n_perm, pi=pis, n_threads=ORACLE_THREADS)
         errs.append(assert_stats_close(res["observed"], obs, what=f"C5 dataset {t} observed"))
         errs.append(assert_stats_close(res["nulls"], exp, what=f"C5 dataset {t} nulls"))
+        # p-values: totalSize = ncol(test) for null = "all" (R/modulePreservation.R:650-654)
+        n_vars = np.array([mi.test_idx[m].size if m in mi.test_idx else 0 for m in modules])
+        pv.append(assert_pvalues_identical(res["nulls"], res["observed"], exp, obs, n_vars, n,
+                                           what=f"C5 dataset {t}"))
         del tcn, tnn, txn
     record("C5 (3 test datasets x 3 perms x 40 modules, null=all, S=1000, k<=2000)", max(errs),
            datasets=3, perms_per_dataset=3)
+    record_pvalues("C5 (3 test datasets x 3 perms x 40 modules x 7 statistics)",
+                   {"count_mismatches": sum(r["count_mismatches"] for r in pv),
+                    "exact_ties": sum(r["exact_ties"] for r in pv),
+                    "closest_nonzero_scaled_gap": min(r["closest_nonzero_scaled_gap"] for r in pv),
+                    "cells": sum(r["cells"] for r in pv)})

@@ -2,9 +2,9 @@
 Lanczos on H = [X' 1]'[X' 1] gives the summary profile u directly
 (src/netStats.cpp:229-236 takes U.col(0) of svd_econ); node contributions
 from one pass over the data. Checked against the C++ LAPACK restatement
-(dgesvd of the S x k block) on identical shuffles, against the primal k x k
-path (NETREP_DUAL_GRAM=0), in vector mode (NetProps' summary profiles) and
-through the non-finite (svd failure) path."""
+(dgesvd of the S x k block) on identical shuffles, in vector mode (NetProps'
+summary profiles), through the non-finite (svd failure) path, and on the
+full-Gram layouts of modules beyond the packed kernel's 320-node layout."""
 import numpy as np
 import pytest
 
@@ -39,12 +39,9 @@ def _cpp(mi, disc, txs, tc, tn, pis):
         np.concatenate([disc["contribution"][m] for m in mods]), pis.shape[0], pi=pis, n_threads=8)
 
 
-@pytest.mark.parametrize("variant", [None, "full"])
-def test_dual_gram_vs_cpp_oracle(variant, monkeypatch):
+def test_dual_gram_vs_cpp_oracle():
     """S = 40 with modules of 20-260 nodes: k > S (dual), k == S and k < S
-    (primal) in one launch; packed (default) and full Gram storage."""
-    if variant:
-        monkeypatch.setenv("NETREP_PROFILE_VARIANT", variant)
+    (primal) in one launch of the packed kernel."""
     lay, mi, disc, txs, tc, tn = _case([260, 180, 64, 41, 40, 39, 20], 40, 5)
     eng = _engine_from(mi, disc, txs, tc, tn)
     nulls = eng.run(10, 22, 99)
@@ -54,15 +51,18 @@ def test_dual_gram_vs_cpp_oracle(variant, monkeypatch):
     assert_stats_close(nulls, exp, what="nulls (dual)")
 
 
-def test_dual_equals_primal(monkeypatch):
-    """The dual and the primal Gram give the same statistics (to rounding)."""
-    lay, mi, disc, txs, tc, tn = _case([200, 120, 70], 60, 9)
+def test_size_classes_vs_cpp_oracle():
+    """Modules beyond the packed kernel's 320-node layout run in their own
+    launch on the full-Gram layout (S = 400 > k: primal, full Gram; k > S:
+    dual), the rest on the packed kernel -- one cube, every statistic at the
+    parity bar."""
+    lay, mi, disc, txs, tc, tn = _case([520, 350, 330, 300, 120, 45], 400, 21)
     eng = _engine_from(mi, disc, txs, tc, tn)
-    a = eng.run(0, 16, 3)
-    monkeypatch.setenv("NETREP_DUAL_GRAM", "0")
-    eng2 = _engine_from(mi, disc, txs, tc, tn)
-    b = eng2.run(0, 16, 3)
-    assert_stats_close(a, b, what="dual vs primal")
+    nulls = eng.run(3, 11, 7)
+    pis = N.prp_table(7, 3, 11, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (size classes)")
+    assert_stats_close(nulls, exp, what="nulls (size classes)")
 
 
 def test_dual_netprops_summary():

@@ -47,3 +47,62 @@ def test_engine_set_dataset_files_names_and_flags(tmp_path, bundled):
     assert names == list(b["test_network_colnames"])
     assert eng.symmetric()
     eng.close()
+
+
+def test_files_node_order_mismatch_rejected(tmp_path, bundled):
+    """R/check-user-input.R:757-771: the correlation, network and data files
+    must list the nodes in one order ("mismatch in node order ..."), and each
+    square matrix's row names must equal its column names."""
+    b = bundled
+    cols = list(b["test_network_colnames"])
+    swapped = cols[1:2] + cols[:1] + cols[2:]
+    pc, pn, pd = (str(tmp_path / f"{x}.rds") for x in ("c", "n", "d"))
+    write_rds(pc, b["test_correlation"], None, swapped)
+    write_rds(pn, b["test_network"], None, cols)
+    eng = N.Engine(0)
+    with pytest.raises(N.NetRepError) as ei:
+        eng.set_dataset_files(pc, pn)
+    assert "node order" in str(ei.value)
+    write_rds(pc, b["test_correlation"], swapped, cols)   # rownames != colnames
+    with pytest.raises(N.NetRepError) as ei:
+        eng.set_dataset_files(pc, pn)
+    assert "row and column names" in str(ei.value)
+    write_rds(pc, b["test_correlation"], None, cols)
+    write_rds(pd, b["test_data"], None, swapped)
+    with pytest.raises(N.NetRepError) as ei:
+        eng.set_dataset_files(pc, pn, pd)
+    assert "node order" in str(ei.value)
+    eng.close()
+
+
+def test_failed_file_load_leaves_no_dataset(tmp_path, bundled):
+    """A load that fails part-way (here: the data file does not match) leaves
+    the context with no dataset, and modules / null pool set for the previous
+    dataset are refused until set again (no stale shapes, no
+    out-of-bounds kernels)."""
+    from test_gpu_parity import bundled_inputs  # noqa: F401
+    b = bundled
+    cols = list(b["test_network_colnames"])
+    pc, pn, pd = (str(tmp_path / f"{x}.rds") for x in ("c", "n", "d"))
+    write_rds(pc, b["test_correlation"], None, cols)
+    write_rds(pn, b["test_network"], None, cols)
+    write_rds(pd, b["test_data"][:, :-1], None, cols[:-1])   # one node short
+    eng = N.Engine(0)
+    eng.set_dataset_files(pc, pn)
+    n = len(cols)
+    idx = np.arange(20, dtype=np.int32)
+    eng.set_modules(1, np.arange(1), np.array([0, 20], dtype=np.int64), idx, idx,
+                    np.zeros(190), np.zeros(20), None)
+    eng.set_null_pool(np.arange(n, dtype=np.int32))
+    eng.run(0, 4, 1)   # works on the good dataset
+    with pytest.raises(N.NetRepError):
+        eng.set_dataset_files(pc, pn, pd)
+    assert eng.shape() == (0, 0)
+    with pytest.raises(N.NetRepError) as ei:
+        eng.run(0, 4, 1)
+    assert "dataset" in str(ei.value)
+    eng.set_dataset_files(pc, pn)      # a new load: modules must be set again
+    with pytest.raises(N.NetRepError) as ei:
+        eng.run(0, 4, 1)
+    assert "nr_set_modules" in str(ei.value)
+    eng.close()

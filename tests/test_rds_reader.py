@@ -78,3 +78,69 @@ def test_reads_the_references_own_rda(tmp_path):
         got = N.read_rds_matrix(p, name)
         np.testing.assert_array_equal(got.values, gold[name])
         assert got.colnames == list(gold[name + "_colnames"])
+
+
+def _forged(path, body_parts):
+    import struct
+    data = b"X\n" + struct.pack(">iii", 2, 0x040301, 0x020300) + b"".join(body_parts)
+    with open(path, "wb") as f:
+        f.write(data)
+
+
+def test_forged_lengths_fail_cleanly(tmp_path):
+    """lengths in an untrusted file are bounded before anything is
+    allocated or skipped -- a forged long-vector length (2^60), a huge string
+    length in the dimnames, and negative dims come back as NetRepError
+    (NR_ERR_INVALID), never std::bad_alloc / std::terminate."""
+    import struct
+    p = str(tmp_path / "long.rds")
+    # REALSXP with a long length of 2^60 (beyond R_XLEN_T_MAX = 2^52)
+    _forged(p, [struct.pack(">iiii", 14 | (1 << 9), -1, 1 << 28, 0)])
+    with pytest.raises(NetRepError) as ei:
+        N.read_rds_matrix(p)
+    assert ei.value.code == 2 and "limit" in str(ei.value)
+    # a 1x1 matrix whose colnames CHARSXP claims 2^31-1 bytes (then EOF)
+    q = str(tmp_path / "str.rds")
+    parts = [struct.pack(">ii", 14 | (1 << 9), 1), struct.pack(">d", 1.0),
+             struct.pack(">i", 2 | (1 << 10)), struct.pack(">i", 1), struct.pack(">ii", 0x00040009, 3), b"dim",
+             struct.pack(">iiii", 13, 2, 1, 1),
+             struct.pack(">i", 2 | (1 << 10)), struct.pack(">i", 1), struct.pack(">ii", 0x00040009, 8), b"dimnames",
+             struct.pack(">ii", 19, 2), struct.pack(">i", 254),
+             struct.pack(">ii", 16, 1), struct.pack(">ii", 0x00040009, 2**31 - 1), b"abc"]
+    _forged(q, parts)
+    with pytest.raises(NetRepError) as ei:
+        N.read_rds_matrix(q)
+    assert ei.value.code == 2
+    # a character vector claiming 2^52 entries
+    r = str(tmp_path / "vec.rds")
+    parts2 = parts[:-2] + [struct.pack(">iiii", 16, -1, 1 << 20, 0)]
+    _forged(r, parts2)
+    with pytest.raises(NetRepError):
+        N.read_rds_matrix(r)
+
+
+def test_negative_dims_rejected(tmp_path):
+    """dim = (-2, -3) with a 6-element payload is not a matrix."""
+    import struct
+    p = str(tmp_path / "neg.rds")
+    parts = [struct.pack(">ii", 14 | (1 << 9), 6), np.arange(6.0).astype(">f8").tobytes(),
+             struct.pack(">i", 2 | (1 << 10)), struct.pack(">i", 1), struct.pack(">ii", 0x00040009, 3), b"dim",
+             struct.pack(">iiii", 13, 2, -2, -3), struct.pack(">i", 254)]
+    _forged(p, parts)
+    with pytest.raises(NetRepError):
+        N.read_rds_matrix(p)
+
+
+def test_altrep_dimnames_reported(tmp_path):
+    """R >= 3.5 ALTREP (compact) dimnames are not decoded; the error says so."""
+    import struct
+    p = str(tmp_path / "alt.rds")
+    parts = [struct.pack(">ii", 14 | (1 << 9), 1), struct.pack(">d", 1.0),
+             struct.pack(">i", 2 | (1 << 10)), struct.pack(">i", 1), struct.pack(">ii", 0x00040009, 3), b"dim",
+             struct.pack(">iiii", 13, 2, 1, 1),
+             struct.pack(">i", 2 | (1 << 10)), struct.pack(">i", 1), struct.pack(">ii", 0x00040009, 8), b"dimnames",
+             struct.pack(">ii", 19, 2), struct.pack(">i", 254), struct.pack(">i", 238)]
+    _forged(p, parts)
+    with pytest.raises(NetRepError) as ei:
+        N.read_rds_matrix(p)
+    assert "ALTREP" in str(ei.value)
