@@ -397,22 +397,26 @@ def run_c5(args, world, rank, local):
     t_setup = time.perf_counter() - t_setup
     P = args.perms_per_step or 256
     K, W = args.steps, args.warmup
+    n_cores = host_cores()["lease_share"]   # nThreads: the lease's host cores stage the uploads
+    N._lib.load().nr_set_host_threads(n_cores)
 
-    def one_pass(step):
-        N.PrefetchTestDataset(*datasets[0])
-        for t in range(3):
-            if t + 1 < 3:
-                N.PrefetchTestDataset(*datasets[t + 1])   # uploads while dataset t runs
-            r = N.PermutationProcedure(disc, *datasets[t], ma, modules, P, nullHypothesis="all",
-                                       seed=seed + 1000 * step + t)
-        return r
-
-    for w in range(W):
-        one_pass(-1 - w)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k_ in range(K):
-        last = one_pass(k_)
+    # modulePreservation's loop over (step, test dataset), pipelined: the next
+    # dataset's upload is started before the current one's permutations
+    order = [(k_, t) for k_ in range(-W, K) for t in range(3)]
+    N.PrefetchTestDataset(*datasets[0])
+    call_s = []
+    t0 = None
+    for i, (k_, t) in enumerate(order):
+        if k_ == 0 and t == 0:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        if i + 1 < len(order):
+            N.PrefetchTestDataset(*datasets[order[i + 1][1]])   # uploads while dataset t runs
+        tc_ = time.perf_counter()
+        last = N.PermutationProcedure(disc, *datasets[t], ma, modules, P, nCores=n_cores, nullHypothesis="all",
+                                      seed=seed + 1000 * k_ + t)
+        if k_ >= 0:
+            call_s.append(round(time.perf_counter() - tc_, 4))
     elapsed = time.perf_counter() - t0
     finite = float(np.isfinite(last["nulls"]).mean())
     # upload alone (pinned double-buffered chunks, 25.9 GB per dataset) and
@@ -457,6 +461,7 @@ def run_c5(args, world, rank, local):
         "compute_s_per_dataset": compute_s,
         "compute_perms_per_sec": P / compute_s,
         "pipelined_s_per_dataset": elapsed / (3 * K),
+        "call_s": call_s,
         "kernels": {"module_net_kernel": {"avg_ms": ms0 / max(l0, 1), "launches": l0},
                     "module_profile_kernel": {"avg_ms": ms1 / max(l1, 1), "launches": l1,
                                               "achieved": prof_f * P / (ms1 * 1e-3) / 1e12 if ms1 > 0 else None,

@@ -183,7 +183,7 @@ int nr_cancel(nr_ctx* ctx);
 /* Tuning and measurement. */
 int nr_set_batch(nr_ctx* ctx, int64_t perms_per_launch);
 /* Host threads of the pinned staging copies (process-wide; n <= 0: 8, the
- * default; capped at 8). The reference-interface calls set it from n_cores. */
+ * default; capped at 16). The reference-interface calls set it from n_cores. */
 int nr_set_host_threads(int n);
 int nr_set_timing(nr_ctx* ctx, int enable);
 /* Accumulated device time (HIP events on the launch stream) per kernel:
@@ -260,7 +260,7 @@ int netrep_format_progress(int64_t done, int64_t total, char* buf, int64_t cap);
  * `pi` (optional, [n_perm x n_null]) supplies explicit shuffles. n_cores
  * (nThreads of the reference, which sizes its worker pool) bounds the host
  * threads the call uses for its own work -- the pinned staging copies of the
- * test matrices (at most min(n_cores, 8) threads; n_cores <= 0: 8); the
+ * test matrices (at most min(n_cores, 16) threads; n_cores <= 0: 8); the
  * permutations themselves run on the GPUs. NETREP_NUM_GPUS selects the GPU count
  * (NETREP_SHARE_DEVICE=1 lets several contexts share the visible GPUs, a test
  * mode for the sharded path on a one-GPU machine). The test matrices are

@@ -359,6 +359,16 @@ __device__ __forceinline__ double nr_wave_max(double v) {
   return nr_swap32_max(nr_swap16_max(v));
 }
 
+// Sum over the 16 lanes of each DPP row (lanes 16r..16r+15); every lane of
+// the row ends with its row's total. Fixed order: bitwise reproducible.
+__device__ __forceinline__ double nr_row_sum16(double v) {
+  v += nr_dpp<NR_DPP_XOR1>(v);
+  v += nr_dpp<NR_DPP_XOR2>(v);
+  v += nr_dpp<NR_DPP_HALF_MIRROR>(v);  // quads are uniform: lane ^ 4
+  v += nr_dpp<NR_DPP_ROR8>(v);
+  return v;
+}
+
 // Lane l's double, broadcast to the wave (two v_readlane_b32: SGPR result).
 __device__ __forceinline__ double nr_readlane_f64(double v, int l) {
   const uint64_t u = __builtin_bit_cast(uint64_t, v);
@@ -530,22 +540,34 @@ __device__ __forceinline__ void profile_contrib_dual(const ProfileParams& P, int
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double Sd = (double)S;
   const double* u = L.vv;
-  for (int c = wave; c < k; c += NW) {
-    const double* col = X + (int64_t)L.idx[c] * S;
-    double a = 0.0, b = 0.0, q = 0.0;
-    for (int s = lane; s < S; s += 64) {
-      const double x = col[s];
-      a = fma(x, u[s], a);
-      b += x;
-      q = fma(x, x, q);
+  // 16 lanes per node, 4 nodes per wave instruction, two node groups in
+  // flight: the column loads of 8 nodes are issued before any is reduced (the
+  // pass was one dependent global round trip per node: 14% of a C2 item)
+  const int g16 = lane >> 4, l16 = lane & 15;
+  for (int c0 = 8 * wave; c0 < k; c0 += 8 * NW) {
+    double a[2] = {0.0, 0.0}, b[2] = {0.0, 0.0}, q[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = c0 + 4 * h + g16;
+      const double* col = X + (int64_t)L.idx[c < k ? c : k - 1] * S;
+      for (int s = l16; s < S; s += 16) {
+        const double x = c < k ? col[s] : 0.0;
+        a[h] = fma(x, u[s], a[h]);
+        b[h] += x;
+        q[h] = fma(x, x, q[h]);
+      }
     }
-    a = wave_sum(a);
-    b = wave_sum(b);
-    q = wave_sum(q);
-    if (lane == 0) {
-      L.gv[c] = a;
-      L.colm[c] = b / Sd;
-      L.q[c] = q;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a[h] = nr_row_sum16(a[h]);
+      b[h] = nr_row_sum16(b[h]);
+      q[h] = nr_row_sum16(q[h]);
+      const int c = c0 + 4 * h + g16;
+      if (l16 == 0 && c < k) {
+        L.gv[c] = a[h];
+        L.colm[c] = b[h] / Sd;
+        L.q[c] = q[h];
+      }
     }
   }
   double a3[1] = {0.0};

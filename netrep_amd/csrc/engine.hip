@@ -744,7 +744,7 @@ const char* nr_last_error(const nr_ctx* ctx) {
 static std::atomic<int> g_host_threads{8};
 
 int nr_set_host_threads(int n) {
-  g_host_threads = n <= 0 ? 8 : std::min(n, 8);
+  g_host_threads = n <= 0 ? 8 : std::min(n, 16);
   return NR_OK;
 }
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
@@ -61,8 +62,10 @@ void run(const void* buf, int64_t n, int blocks, int threads, int iters, double*
          threads, cw, ms, reads / (ms * 1e-3) / 1e9, reads * sizeof(T) / (ms * 1e-3) / 1e9);
 }
 
-int main() {
-  const int64_t n = 20000;
+int main(int argc, char** argv) {
+  // N = 20,000 (C3/C4: 6.4 GB) by default; 40,000 for C5's 25.6 GB footprint
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 20000;
+  printf("N = %lld (%.1f GB interleaved)\n", (long long)n, (double)(n * n) * 16 / 1e9);
   void* buf = nullptr;
   if (hipMalloc(&buf, (size_t)(n * n) * 16) != hipSuccess) return 1;
   hipMemset(buf, 0, (size_t)(n * n) * 16);
@@ -79,6 +82,11 @@ int main() {
   // one 512-thread block per CU, 4 in flight (the fused profile kernel's budget)
   run<4, double2>(buf, n, 256, 512, 64, out, "16B/1wg");
   run<8, double2>(buf, n, 256, 512, 32, out, "16B/1wg");
+  // fewer workgroups: the parallelism of a launch tail of large modules
+  // (C5's k >= 1,000 items run one or two workgroups per CU)
+  run<7, double2>(buf, n, 512, 256, 64, out, "16B/2wg");
+  run<7, double2>(buf, n, 256, 256, 128, out, "16B/1wg4");
+  run<7, double2>(buf, n, 256, 128, 128, out, "16B/1wg2");
   for (uint32_t cw : {1024u, 512u, 256u, 128u, 64u, 16u}) run<8, double2>(buf, n, 2048, 256, 32, out, "16B", cw);
   return 0;
 }
