@@ -122,6 +122,16 @@ int nr_set_null_pool(nr_ctx* ctx, const int32_t* null_idx, int64_t n_null);
  * 4 without. */
 int nr_observed(nr_ctx* ctx, double* observed);
 
+/* The same, split so that it runs beside the permutations: nr_observed_async
+ * enqueues the observed launch on the context's second stream (its own
+ * scratch and work queue) and returns; nr_run / nr_run_device may follow at
+ * once, and their first batch shares the GPU with it. nr_observed_wait
+ * copies the statistics out (blocking). Any change of dataset, modules or
+ * null pool in between waits for the launch and discards it (nr_observed_wait
+ * then returns NR_ERR_INVALID). */
+int nr_observed_async(nr_ctx* ctx);
+int nr_observed_wait(nr_ctx* ctx, double* observed);
+
 /* Null distributions for global permutations [perm_begin, perm_end).
  * pi == NULL: permutation p draws pi_p = keyed PRP(seed, p) (prp.h).
  * pi != NULL: explicit host table [(perm_end-perm_begin) x n_null] of

@@ -20,6 +20,7 @@ computed on the CPU.
 from __future__ import annotations
 
 import ctypes as C
+from collections import OrderedDict
 import sys
 from dataclasses import dataclass
 from typing import Mapping, Optional, Sequence
@@ -47,9 +48,23 @@ class RMatrix:
         return np.asfortranarray(np.asarray(self.values, dtype=np.float64))
 
 
+_STRV_CACHE: "OrderedDict[tuple, tuple]" = OrderedDict()
+
+
 def _strv(names: Sequence[str]):
-    enc = [str(n).encode() for n in names]
+    """A char** of `names` (and the bytes it points into). The last few name
+    lists are kept: modulePreservation passes the same node names and module
+    assignments on every call (C5: 100k strings, ~60 ms to re-encode)."""
+    key = tuple(str(n) for n in names)
+    hit = _STRV_CACHE.get(key)
+    if hit is not None:
+        _STRV_CACHE.move_to_end(key)
+        return hit
+    enc = [n.encode() for n in key]
     arr = (C.c_char_p * max(len(enc), 1))(*enc)
+    _STRV_CACHE[key] = (arr, enc)
+    while len(_STRV_CACHE) > 8:
+        _STRV_CACHE.popitem(last=False)
     return arr, enc
 
 

@@ -87,6 +87,26 @@ struct nr_ctx {
   size_t net_scratch_cap = 0;
   int* d_counters = nullptr;  // [0] queue head, [1..4] lanczos diagnostics, [5] flag
   int64_t batch = 0;          // 0 = automatic
+  // the second output / staging buffer of run_impl's two batches in flight
+  double* d_out2 = nullptr;
+  size_t out2_cap = 0;
+  double* h_stage2 = nullptr;
+  size_t stage2_cap = 0;
+  hipEvent_t ev_copy[2] = {nullptr, nullptr};
+
+  // The observed statistics' own lane (nr_observed_async): stream, scratch and
+  // work queue, so that they run beside the first permutation batch instead
+  // of ahead of it (at C5 the one-item-per-module launch held the GPU ~85 ms
+  // per PermutationProcedure call with 40 workgroups busy).
+  hipStream_t obs_stream = nullptr;
+  double* obs_scratch = nullptr;
+  size_t obs_scratch_cap = 0;
+  double* obs_net_scratch = nullptr;
+  size_t obs_net_cap = 0;
+  int* obs_counters = nullptr;
+  double* d_obs = nullptr;
+  size_t obs_cap = 0;
+  bool obs_pending = false;  // cleared by every change of dataset, modules or null pool
 
   std::atomic<int64_t> done{0}, total{0};
   std::atomic<bool> cancel{false};
@@ -140,12 +160,12 @@ int ensure(nr_ctx* ctx, T*& buf, size_t& cap, size_t n) {
   return NR_OK;
 }
 
-int ensure_stage(nr_ctx* ctx, size_t n) {
-  if (n <= ctx->stage_cap && ctx->h_stage) return NR_OK;
-  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-  ctx->h_stage = nullptr;
-  NR_HIP(ctx, hipHostMalloc((void**)&ctx->h_stage, n * sizeof(double), hipHostMallocDefault));
-  ctx->stage_cap = n;
+int ensure_stage(nr_ctx* ctx, double*& h, size_t& cap, size_t n) {
+  if (n <= cap && h) return NR_OK;
+  if (h) (void)hipHostFree(h);
+  h = nullptr;
+  NR_HIP(ctx, hipHostMalloc((void**)&h, n * sizeof(double), hipHostMallocDefault));
+  cap = n;
   return NR_OK;
 }
 
@@ -171,10 +191,10 @@ int fill_virtual_columns(nr_ctx* ctx, int64_t n_nodes, int64_t n_samples) {
   return NR_OK;
 }
 
-int fill_na(nr_ctx* ctx, double* d, int64_t n) {
+int fill_na(nr_ctx* ctx, double* d, int64_t n, hipStream_t st = nullptr) {
   if (n <= 0) return NR_OK;
   const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(na_fill_kernel, dim3(g), dim3(256), 0, ctx->stream, d, n);
+  hipLaunchKernelGGL(na_fill_kernel, dim3(g), dim3(256), 0, st ? st : ctx->stream, d, n);
   NR_HIP(ctx, hipGetLastError());
   return NR_OK;
 }
@@ -184,7 +204,16 @@ int n_stat_of(const nr_ctx* ctx) { return ctx->d_data ? NR_NSTAT_DATA : NR_NSTAT
 // No dataset: buffers freed, shape zero. Modules validated against an earlier
 // dataset (their node indices) stop being usable: check_ready demands a new
 // nr_set_modules after any dataset change.
+// Wait for an observed launch still running on the second lane (before its
+// inputs are replaced or freed) and drop its result: nr_observed_wait then
+// refuses until nr_observed_async is called again.
+void sync_obs(nr_ctx* ctx) {
+  if (ctx->obs_stream) (void)hipStreamSynchronize(ctx->obs_stream);
+  ctx->obs_pending = false;
+}
+
 void reset_dataset(nr_ctx* ctx) {
+  sync_obs(ctx);
   dfree(ctx->d_pairs);
   dfree(ctx->d_data);
   ctx->node_names.clear();
@@ -319,6 +348,29 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   return NR_OK;
 }
 
+// The device resources one stream of launches uses: the permutation batches
+// run on the context's own (main_lane), the observed statistics of a
+// PermutationProcedure call on a second set (obs_lane) beside them.
+struct Lane {
+  hipStream_t st;
+  double** scratch;
+  size_t* scratch_cap;
+  double** net_scratch;
+  size_t* net_cap;
+  int* counters;  // [0] queue head, [1..4] Lanczos diagnostics
+  bool timed;     // kernel timers (nr_set_timing) follow the main lane only
+};
+
+Lane main_lane(nr_ctx* ctx) {
+  return {ctx->stream, &ctx->d_scratch, &ctx->scratch_cap, &ctx->d_net_scratch, &ctx->net_scratch_cap,
+          ctx->d_counters, true};
+}
+
+Lane obs_lane(nr_ctx* ctx) {
+  return {ctx->obs_stream, &ctx->obs_scratch, &ctx->obs_scratch_cap, &ctx->obs_net_scratch, &ctx->obs_net_cap,
+          ctx->obs_counters, false};
+}
+
 // Summary-profile launches over the module order sorted by size (descending,
 // k_sorted[i] = size of d_order[i]), one per size class, each with its own
 // work queue, k_max and layout: the modules beyond the packed kernel's
@@ -327,7 +379,8 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
 // module on the layout of the largest one: at C5 the small modules ran on the
 // one-workgroup-per-CU full-Gram kernel too.)
 int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
-                    const std::vector<int32_t>& k_sorted, int64_t n_perm, hipStream_t st) {
+                    const std::vector<int32_t>& k_sorted, int64_t n_perm, const Lane& ln) {
+  const hipStream_t st = ln.st;
   const int n_mod = (int)k_sorted.size();
   int n_big = 0;
   while (n_big < n_mod && k_sorted[n_big] > nr::kPackedLayoutK) ++n_big;
@@ -347,7 +400,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     total = std::max<int64_t>(total, seg[i].plan.stride * seg[i].plan.slots);
   }
   // segments run one after the other on one stream: they share the scratch
-  if (int rc = ensure(ctx, ctx->d_scratch, ctx->scratch_cap, (size_t)total)) return rc;
+  if (int rc = ensure(ctx, *ln.scratch, *ln.scratch_cap, (size_t)total)) return rc;
   for (int i = 0; i < ns; ++i) {
     const ProfilePlan& plan = seg[i].plan;
     const int k_max = k_sorted[seg[i].first];
@@ -359,7 +412,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.kvec = plan.kvec;
     pp.basis_doubles = plan.basis_doubles;
     pp.gram_doubles = plan.gram_doubles;
-    pp.scratch = ctx->d_scratch;
+    pp.scratch = *ln.scratch;
     pp.scratch_stride = plan.stride;
     pp.part_global = plan.variant == 4 ? 1 : 0;
     pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples);
@@ -412,15 +465,15 @@ nr::IndexSource make_source(const nr_ctx* ctx, int mode, uint64_t seed, int64_t 
 
 // Network kernel scratch for modules whose per-node arrays exceed LDS: a
 // persistent grid of two workgroups per CU, each with its own slot.
-int prepare_net(nr_ctx* ctx, nr::NetParams& np, int64_t n_items) {
+int prepare_net(nr_ctx* ctx, nr::NetParams& np, int64_t n_items, const Lane& ln) {
   if (!nr::net_kernel_big(np.k_max)) return NR_OK;
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
   const int64_t slots = std::max<int64_t>(1, std::min<int64_t>(n_items, 2 * (int64_t)dev_cu));
   const int64_t per = (int64_t)(nr::net_big_slot_bytes(np.k_max) / sizeof(double));
-  const int rc = ensure(ctx, ctx->d_net_scratch, ctx->net_scratch_cap, (size_t)(per * slots));
+  const int rc = ensure(ctx, *ln.net_scratch, *ln.net_cap, (size_t)(per * slots));
   if (rc) return rc;
-  np.big_scratch = ctx->d_net_scratch;
+  np.big_scratch = *ln.net_scratch;
   np.big_stride = per;
   np.big_slots = (int32_t)slots;
   return NR_OK;
@@ -430,7 +483,7 @@ int prepare_net(nr_ctx* ctx, nr::NetParams& np, int64_t n_items) {
 // whose per-node arrays do not fit LDS first (global-scratch workgroups), the
 // rest in the ordinary one-workgroup-per-item launch with their own k_max.
 int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std::vector<int32_t>& k_sorted,
-                int64_t n_perm, hipStream_t st) {
+                int64_t n_perm, const Lane& ln) {
   const int n_mod = (int)k_sorted.size();
   int n_big = 0;
   while (n_big < n_mod && nr::net_kernel_big(k_sorted[n_big])) ++n_big;
@@ -441,20 +494,20 @@ int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std
     q.mod_order = d_order + first[i];
     q.k_max = k_sorted[first[i]];
     const int64_t items = (int64_t)count[i] * n_perm;
-    const int rc = prepare_net(ctx, q, items);
+    const int rc = prepare_net(ctx, q, items, ln);
     if (rc) return rc;
-    NR_HIP(ctx, nr::launch_net(q, items, st));
+    NR_HIP(ctx, nr::launch_net(q, items, ln.st));
   }
   return NR_OK;
 }
 
 // Launch the statistics kernels for n_perm permutations (or the observed /
 // direct sets when src.mode == NR_IDX_DIRECT, n_perm == 1) into d_out.
-int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double* d_out) {
+int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double* d_out, const Lane& ln) {
   const int n_stat = n_stat_of(ctx);
   const bool data = ctx->d_data != nullptr;
   NR_HIP(ctx, hipSetDevice(ctx->device));
-  int rc = fill_na(ctx, d_out, (int64_t)ctx->n_rows * n_stat * n_perm);
+  int rc = fill_na(ctx, d_out, (int64_t)ctx->n_rows * n_stat * n_perm, ln.st);
   if (rc) return rc;
   if (ctx->n_present == 0) return NR_OK;
   const int64_t n_items = (int64_t)ctx->n_present * n_perm;
@@ -485,9 +538,9 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   // the summary-profile launches, on the same stream. (Round 2 measured the
   // network phase fused into the profile items at +0.7%, within run-to-run
   // noise, and on a concurrent stream at -11%: profiles/r02/profile_variants.txt.)
-  timer_begin(ctx, 0, ctx->stream);
-  if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ctx->order_k_h, n_perm, ctx->stream))) return rc;
-  timer_end(ctx, 0, n_items, ctx->stream);
+  if (ln.timed) timer_begin(ctx, 0, ln.st);
+  if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ctx->order_k_h, n_perm, ln))) return rc;
+  if (ln.timed) timer_end(ctx, 0, n_items, ln.st);
 
   if (data) {
     nr::ProfileParams pp{};
@@ -505,15 +558,15 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.slot_cor_contrib = 4;
     pp.slot_avg_contrib = 6;
     pp.out = d_out;
-    pp.queue = ctx->d_counters;
-    pp.diag = ctx->d_counters + 1;
-    pp.stamps = ctx->d_stamps;
-    timer_begin(ctx, 1, ctx->stream);
-    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ctx->stream);
+    pp.queue = ln.counters;
+    pp.diag = ln.counters + 1;
+    pp.stamps = ln.timed ? ctx->d_stamps : nullptr;
+    if (ln.timed) timer_begin(ctx, 1, ln.st);
+    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ln);
     if (rc) return rc;
-    timer_end(ctx, 1, n_items, ctx->stream);
+    if (ln.timed) timer_end(ctx, 1, n_items, ln.st);
   }
-  timer_collect(ctx);
+  if (ln.timed) timer_collect(ctx);
   return NR_OK;
 }
 
@@ -620,8 +673,31 @@ int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* p
     }
     return fail(ctx, NR_ERR_CANCELLED, "permutation procedure cancelled");
   };
-  for (int64_t p0 = b; p0 < e; p0 += batch) {
-    if (ctx->cancel.load()) return cancelled(p0);
+  // Host output: two batches in flight. Batch i+1 is enqueued behind batch
+  // i's copy to pinned memory, so the device does not idle while the host
+  // moves batch i's slices into `nulls` (drain).
+  struct Pending {
+    int64_t p0 = -1, np = 0;
+    int slot = 0;
+  } pend;
+  double* h_slot[2] = {nullptr, nullptr};
+  auto drain = [&]() -> int {
+    if (pend.p0 < 0) return NR_OK;
+    NR_HIP(ctx, hipEventSynchronize(ctx->ev_copy[pend.slot]));
+    std::memcpy(nulls + (pend.p0 - b) * slice, h_slot[pend.slot], (size_t)(pend.np * slice) * sizeof(double));
+    ctx->done += pend.np;
+    pend.p0 = -1;
+    return NR_OK;
+  };
+  if (!nulls_on_device)
+    for (auto& ev : ctx->ev_copy)
+      if (!ev) NR_HIP(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  int slot = 0;
+  for (int64_t p0 = b; p0 < e; p0 += batch, slot ^= 1) {
+    if (ctx->cancel.load()) {
+      if ((rc = drain())) return rc;
+      return cancelled(p0);
+    }
     const int64_t np = std::min(batch, e - p0);
     const uint32_t* d_pi = nullptr;
     if (pi) {
@@ -642,24 +718,31 @@ int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* p
     if (nulls_on_device) {
       d_out = nulls + (p0 - b) * slice;
     } else {
-      rc = ensure(ctx, ctx->d_out, ctx->out_cap, (size_t)(np * slice));
+      rc = slot == 0 ? ensure(ctx, ctx->d_out, ctx->out_cap, (size_t)(np * slice))
+                     : ensure(ctx, ctx->d_out2, ctx->out2_cap, (size_t)(np * slice));
       if (rc) return rc;
-      d_out = ctx->d_out;
+      d_out = slot == 0 ? ctx->d_out : ctx->d_out2;
     }
-    rc = launch_batch(ctx, src, np, d_out);
+    rc = launch_batch(ctx, src, np, d_out, main_lane(ctx));
     if (rc) return rc;
     if (!nulls_on_device) {
-      rc = ensure_stage(ctx, (size_t)(np * slice));
+      rc = slot == 0 ? ensure_stage(ctx, ctx->h_stage, ctx->stage_cap, (size_t)(np * slice))
+                     : ensure_stage(ctx, ctx->h_stage2, ctx->stage2_cap, (size_t)(np * slice));
       if (rc) return rc;
-      NR_HIP(ctx, hipMemcpyAsync(ctx->h_stage, d_out, (size_t)(np * slice) * sizeof(double),
+      h_slot[slot] = slot == 0 ? ctx->h_stage : ctx->h_stage2;
+      NR_HIP(ctx, hipMemcpyAsync(h_slot[slot], d_out, (size_t)(np * slice) * sizeof(double),
                                  hipMemcpyDeviceToHost, ctx->stream));
-      NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
-      std::memcpy(nulls + (p0 - b) * slice, ctx->h_stage, (size_t)(np * slice) * sizeof(double));
+      NR_HIP(ctx, hipEventRecord(ctx->ev_copy[slot], ctx->stream));
+      if ((rc = drain())) return rc;   // the previous batch, while this one runs
+      pend.p0 = p0;
+      pend.np = np;
+      pend.slot = slot;
     } else {
       NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      ctx->done += np;
     }
-    ctx->done += np;
   }
+  if ((rc = drain())) return rc;
   ctx->cancel = false;  // a cancellation that arrives after the last launch has nothing left to stop
   return NR_OK;
 }
@@ -709,6 +792,7 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  sync_obs(ctx);
   dfree(ctx->d_pairs);
   dfree(ctx->d_data);
   dfree(ctx->d_row_of);
@@ -728,9 +812,18 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   dfree(ctx->d_net_scratch);
   dfree(ctx->d_counters);
   dfree(ctx->d_stamps);
+  dfree(ctx->d_out2);
+  dfree(ctx->obs_scratch);
+  dfree(ctx->obs_net_scratch);
+  dfree(ctx->obs_counters);
+  dfree(ctx->d_obs);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_stage2) (void)hipHostFree(ctx->h_stage2);
   for (auto& ev : ctx->ev)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : ctx->ev_copy)
+    if (ev) (void)hipEventDestroy(ev);
+  if (ctx->obs_stream) (void)hipStreamDestroy(ctx->obs_stream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1079,6 +1172,7 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
     return fail(ctx, NR_ERR_INVALID, "module arrays missing");
   NR_HIP(ctx, hipSetDevice(ctx->device));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  sync_obs(ctx);
   ctx->modules_gen = -1;  // usable only once everything below has succeeded
   ctx->n_rows = n_rows;
   ctx->n_present = n_present;
@@ -1147,6 +1241,8 @@ int nr_set_null_pool(nr_ctx* ctx, const int32_t* null_idx, int64_t n_null) {
     if (null_idx[i] < 0 || null_idx[i] >= ctx->n_nodes)
       return fail(ctx, NR_ERR_INVALID, "null_idx outside the resident dataset");
   NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  sync_obs(ctx);
   ctx->n_null = n_null;
   int rc = upload(ctx, ctx->d_null_idx, null_idx, (size_t)n_null);
   if (rc) return rc;
@@ -1163,11 +1259,45 @@ int nr_observed(nr_ctx* ctx, double* observed) {
   rc = ensure(ctx, ctx->d_out, ctx->out_cap, (size_t)slice);
   if (rc) return rc;
   const nr::IndexSource src = make_source(ctx, nr::NR_IDX_DIRECT, 0, 0, nullptr, ctx->d_test_idx);
-  rc = launch_batch(ctx, src, 1, ctx->d_out);
+  rc = launch_batch(ctx, src, 1, ctx->d_out, main_lane(ctx));
   if (rc) return rc;
   NR_HIP(ctx, hipMemcpyAsync(observed, ctx->d_out, (size_t)slice * sizeof(double),
                              hipMemcpyDeviceToHost, ctx->stream));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return NR_OK;
+}
+
+int nr_observed_async(nr_ctx* ctx) {
+  if (!ctx) return NR_ERR_INVALID;
+  int rc = check_ready(ctx, false);
+  if (rc) return rc;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  if (!ctx->obs_stream) {
+    NR_HIP(ctx, hipStreamCreateWithFlags(&ctx->obs_stream, hipStreamNonBlocking));
+    NR_HIP(ctx, hipMalloc((void**)&ctx->obs_counters, 16 * sizeof(int)));
+    NR_HIP(ctx, hipMemset(ctx->obs_counters, 0, 16 * sizeof(int)));
+  }
+  sync_obs(ctx);  // a previous observed launch is done before its buffers are reused
+  const int64_t slice = (int64_t)ctx->n_rows * n_stat_of(ctx);
+  rc = ensure(ctx, ctx->d_obs, ctx->obs_cap, (size_t)std::max<int64_t>(slice, 1));
+  if (rc) return rc;
+  const nr::IndexSource src = make_source(ctx, nr::NR_IDX_DIRECT, 0, 0, nullptr, ctx->d_test_idx);
+  rc = launch_batch(ctx, src, 1, ctx->d_obs, obs_lane(ctx));
+  if (rc) return rc;
+  ctx->obs_pending = true;
+  return NR_OK;
+}
+
+int nr_observed_wait(nr_ctx* ctx, double* observed) {
+  if (!ctx || !observed) return NR_ERR_INVALID;
+  if (!ctx->obs_pending)
+    return fail(ctx, NR_ERR_INVALID, "no observed statistics pending (call nr_observed_async after the last "
+                                     "change of dataset, modules or null pool)");
+  ctx->obs_pending = false;
+  const int64_t slice = (int64_t)ctx->n_rows * n_stat_of(ctx);
+  NR_HIP(ctx, hipMemcpyAsync(observed, ctx->d_obs, (size_t)slice * sizeof(double), hipMemcpyDeviceToHost,
+                             ctx->obs_stream));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->obs_stream));
   return NR_OK;
 }
 
@@ -1270,7 +1400,7 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
     np.avgw_out = d_aw;
     std::vector<int32_t> k_sorted(n_mod);
     for (int i = 0; i < n_mod; ++i) k_sorted[i] = (int32_t)(node_off[order[i] + 1] - node_off[order[i]]);
-    if ((rc = launch_nets(ctx, np, d_order, k_sorted, 1, ctx->stream))) break;
+    if ((rc = launch_nets(ctx, np, d_order, k_sorted, 1, main_lane(ctx)))) break;
     e = hipSuccess;
     if (ctx->d_data && (contribution || summary || coherence)) {
       nr::ProfileParams pp{};
@@ -1285,7 +1415,7 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
       pp.coh_out = d_coh;
       pp.queue = ctx->d_counters;
       pp.diag = ctx->d_counters + 1;
-      if ((rc = launch_profiles(ctx, pp, d_order, k_sorted, 1, ctx->stream))) break;
+      if ((rc = launch_profiles(ctx, pp, d_order, k_sorted, 1, main_lane(ctx)))) break;
     }
     auto d2h = [&](double* h, const double* d, int64_t n) {
       if (e == hipSuccess && h && n > 0)

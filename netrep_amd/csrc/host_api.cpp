@@ -192,8 +192,20 @@ struct ModuleSets {
   std::vector<int64_t> node_off{0};
   std::vector<int32_t> test_idx, null_pos;
   std::vector<int32_t> null_idx;
-  std::vector<double> disc_cv, disc_wd, disc_nc;
+  std::vector<double>& disc_cv;  // the calling thread's reused buffer (cv_buffer)
+  std::vector<double> disc_wd, disc_nc;
+  explicit ModuleSets(std::vector<double>& cv) : disc_cv(cv) { disc_cv.clear(); }
 };
+
+// The concatenated discovery correlations of one call (C5: 10.3M doubles)
+// live in a per-thread buffer that keeps its pages between calls:
+// modulePreservation calls PermutationProcedure once per test dataset with
+// the same discovery vectors, and a fresh 82 MB vector per call cost ~40 ms
+// of page faults and copies.
+std::vector<double>& cv_buffer() {
+  thread_local std::vector<double> buf;
+  return buf;
+}
 
 }  // namespace
 
@@ -287,7 +299,7 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
   const ModMap present = make_mod_map(ma_names, ma_labels, n_assign, &t_idx_map);
 
   // MakeNullMap (src/utils.cpp:108-136) over validNodes (src/permutations.cpp:319-323)
-  ModuleSets ms;
+  ModuleSets ms(cv_buffer());
   NameMap null_map;
   {
     const char* const* valid = null_type == "overlap" ? ma_names : t_names;
@@ -301,6 +313,20 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
   }
 
   ms.n_rows = (int32_t)n_modules;
+  {  // one allocation per vector
+    int64_t n_node = 0, n_pair = 0;
+    for (int64_t mi = 0; mi < n_modules; ++mi) {
+      const std::vector<std::string>* nodes = present.find(modules[mi]);
+      const int64_t k = nodes ? (int64_t)nodes->size() : 0;
+      n_node += k;
+      n_pair += k * (k - 1) / 2;
+    }
+    ms.test_idx.reserve((size_t)n_node);
+    ms.null_pos.reserve((size_t)n_node);
+    ms.disc_wd.reserve((size_t)n_node);
+    if (with_data) ms.disc_nc.reserve((size_t)n_node);
+    ms.disc_cv.reserve((size_t)n_pair);
+  }
   for (int64_t mi = 0; mi < n_modules; ++mi) {
     const std::vector<std::string>* nodes = present.find(modules[mi]);
     if (!nodes || nodes->empty()) continue;  // modsPresent (src/permutations.cpp:196-201)
@@ -365,12 +391,18 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
   for (int g = 0; g < n_gpu; ++g)
     if (rcs[g]) return ctx_err(rcs[g], ctxs[g].get());
 
-  // Observed statistics (src/permutations.cpp:246-285).
+  // Observed statistics (src/permutations.cpp:246-285): enqueued on GPU 0's
+  // second stream, where they run beside the first permutation batch, and
+  // collected after the permutations.
   {
-    const int rc = nr_observed(ctxs[0].get(), observed_out);
+    const int rc = nr_observed_async(ctxs[0].get());
     if (rc) return ctx_err(rc, ctxs[0].get());
   }
-  if (n_perm == 0) return NR_OK;  // src/permutations.cpp:288-299
+  auto collect_observed = [&]() -> int {
+    const int rc = nr_observed_wait(ctxs[0].get(), observed_out);
+    return rc ? ctx_err(rc, ctxs[0].get()) : NR_OK;
+  };
+  if (n_perm == 0) return collect_observed();  // src/permutations.cpp:288-299
 
   // Contiguous permutation chunks, remainder to the first devices
   // (src/permutations.cpp:338-354).
@@ -419,6 +451,7 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
   }
   if (verbose) progress_event(NETREP_PROGRESS_END, n_perm, n_perm);
   for (auto& t : th) t.join();
+  if (int rc = collect_observed()) return rc;
   int cancelled_at = -1;
   for (int g = 0; g < n_gpu; ++g) {
     if (rcs[g] == NR_ERR_CANCELLED) {

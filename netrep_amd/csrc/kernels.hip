@@ -163,14 +163,138 @@ __device__ __forceinline__ double wd_final(const NetLds& L, int NWn, int c, int 
 // cor.degree, avg.cor (CorrVector + WeightedDegree gathers, src/netStats.cpp:
 // 124-204; src/permutations.cpp:75-97). One NW-wave workgroup per item. The
 // k(k-1)/2 pairs (column-major lower triangle of the unsorted module order,
-// CorrVector's order) are cut into chunks of CH consecutive pairs dealt
-// round-robin to the threads; a thread walks its chunk with U random 16-byte
-// gathers in flight, keeps the column's (target jj) weighted-degree parts in
-// registers and flushes them at a column change, and adds the row node's
-// (target ii) parts in LDS, where the targets of one wave instruction are
-// distinct (no same-address atomics). L.idx holds the item's test columns.
+// CorrVector's order) are cut into chunks of U consecutive pairs dealt
+// round-robin to the threads; a thread gathers a chunk's U random 16-byte
+// pairs at once (net_issue), keeps the column's (target jj) weighted-degree
+// parts in registers and flushes them at a column change, and adds the row
+// node's (target ii) parts in LDS, where the targets of one wave instruction
+// are distinct (no same-address atomics) (net_process). L.idx holds the
+// item's test columns.
+//
+// PIPE (the two-wave workgroups of modules too large for four waves' LDS
+// copies, one workgroup per CU): the next chunk's gathers are issued before
+// the current chunk is processed, so every lane keeps U gathers in flight
+// through its LDS work -- with two waves per CU nothing else hides it.
 // ---------------------------------------------------------------------------
-template <int NW, int U = 7, int CH = 7>
+// a global (not constant) cell, so the discovery-load pointer stays a global pointer
+__device__ double kNetNanCell = __builtin_nan("");
+
+template <int U>
+struct NetChunk {
+  double2 e[U];   // {corr, net}(idx[ii], idx[jj])
+  double e2[U];   // net(idx[jj], idx[ii])
+  double x[U];    // the discovery correlation of the pair
+  int iis[U];     // row node (-1: past the end)
+  int jjs[U];     // column node
+  int64_t v0;     // the chunk's first pair
+  int j0;         // its column
+};
+
+// Every lane issues all U (2U when the network is not symmetric) gathers and
+// U discovery loads whatever its chunk holds -- entries past the item's end
+// read the item's first diagonal pair and first discovery value -- so the
+// number of loads in flight is the same on every path and the compiler's
+// wait counts can leave the next chunk's gathers outstanding (PIPE).
+template <int U, bool SYM>
+__device__ __forceinline__ void net_issue(const NetParams& P, const NetLds& L, int64_t k, int64_t cvo,
+                                          int64_t npairs, int64_t ch, NetChunk<U>& c) {
+  const double2* __restrict__ pairs = P.pairs;
+  const int64_t n = P.n_nodes;
+  const int64_t v0 = ch * U;
+  const int64_t v1 = v0 + U < npairs ? v0 + U : npairs;
+  // no discovery vector (observed / vector runs): every x reads the NaN cell
+  const double* __restrict__ xp = P.disc_cv ? P.disc_cv + cvo : &kNetNanCell;
+  const int64_t xstep = P.disc_cv ? 1 : 0;
+  int64_t jj64, ii64;
+  decode_pair(v0, k, jj64, ii64);
+  int jj = (int)jj64, ii = (int)ii64;
+  c.v0 = v0;
+  c.j0 = jj;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t v = v0 + u;
+    const bool ok = v < v1;
+    c.iis[u] = ok ? ii : -1;
+    c.jjs[u] = jj;
+    const int64_t r = L.idx[ok ? ii : 0], cc = L.idx[ok ? jj : 0];
+    c.e[u] = pairs[r + cc * n];                 // corr(idx[ii], idx[jj]), net(idx[ii], idx[jj])
+    c.e2[u] = SYM ? c.e[u].y : pairs[cc + r * n].y;   // net(idx[jj], idx[ii])
+    c.x[u] = xp[(ok ? v : v0) * xstep];
+    if (ok && ++ii == k) {
+      ++jj;
+      ii = jj + 1;
+    }
+  }
+}
+
+template <int U, bool STORE>
+__device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L, double* plain_w, int64_t cvo,
+                                            double xs, double ys, const NetChunk<U>& c, double* acc) {
+  // the column's parts, in registers until the column changes
+  int jc = c.j0;
+  int pj = L.rk[jc];
+  int gj = L.ge[jc];
+  double cpl = 0.0, cff = 0.0;
+  unsigned long long cpb = 0, con = 0, ctn = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (c.iis[u] >= 0) {
+      const int i = c.iis[u], j = c.jjs[u];
+      if (j != jc) {  // the chunk crossed into column j: flush the previous column
+        atomicAdd(&plain_w[jc], cpl);
+        if (gj != WD_NO_GRID) {
+          atomicAdd(&L.pb[jc], cpb);
+          atomicAdd(&L.on[jc], con);
+          atomicAdd(&L.tn[jc], ctn);
+          atomicAdd(&L.ff[jc], cff);
+        }
+        cpl = cff = 0.0;
+        cpb = con = ctn = 0;
+        jc = j;
+        pj = L.rk[j];
+        gj = L.ge[j];
+      }
+      const double y = c.e[u].x;
+      if (STORE) P.cv_out[cvo + c.v0 + u] = y;
+      const int pi = L.rk[i];
+      // target jj (column idx[jj]) gains row idx[ii]: registers
+      const double a = fabs(c.e[u].y);
+      cpl += a;
+      if (gj != WD_NO_GRID && isfinite(a)) {
+        if (((pj ^ pi) & 1) == 0) {
+          if (pi < pj) cpb += wd_fx(a, gj, WD_FX_BITS);
+          else if (pi == pj + 2) cff += a;
+          else ctn += wd_fx(a, gj, 0);
+        } else {
+          con += wd_fx(a, gj, WD_FX_BITS);
+        }
+      }
+      // target ii (column idx[ii]) gains row idx[jj]: LDS
+      wd_add(L, plain_w, i, pi, pj, fabs(c.e2[u]));
+      const double xv = c.x[u];
+      if (isfinite(xv) && isfinite(y)) {        // CompleteCases src/netStats.cpp:43-61
+        const double dx = xv - xs, dy = y - ys;
+        acc[0] += 1.0;
+        acc[1] += dx;
+        acc[2] += dy;
+        acc[3] += dx * dx;
+        acc[4] += dy * dy;
+        acc[5] += dx * dy;
+        acc[6] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
+      }
+    }
+  }
+  // flush the last column of the chunk
+  atomicAdd(&plain_w[jc], cpl);
+  if (gj != WD_NO_GRID) {
+    atomicAdd(&L.pb[jc], cpb);
+    atomicAdd(&L.on[jc], con);
+    atomicAdd(&L.tn[jc], ctn);
+    atomicAdd(&L.ff[jc], cff);
+  }
+}
+
+template <int NW, bool PIPE, bool SYM, int U = 7>
 __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_local, int64_t off, int64_t k,
                                          const NetLds& L) {
   constexpr int BS = NW * 64;
@@ -210,102 +334,38 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   const double ys = isfinite(y0) ? y0 : 0.0;
 
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // n, sx, sy, sxx, syy, sxy, s(sign(x) y)
-  const int64_t nchunks = (npairs + CH - 1) / CH;
-  for (int64_t ch = tid; ch < nchunks; ch += BS) {
-    const int64_t v0 = ch * CH;
-    const int64_t v1 = v0 + CH < npairs ? v0 + CH : npairs;
-    int64_t jj64, ii64;
-    decode_pair(v0, k, jj64, ii64);
-    int jj = (int)jj64, ii = (int)ii64;
-    // the column's parts, in registers until the column changes
-    int pj = L.rk[jj];
-    int gj = L.ge[jj];
-    double cpl = 0.0, cff = 0.0;
-    unsigned long long cpb = 0, con = 0, ctn = 0;
-    for (int64_t vb = v0; vb < v1; vb += U) {
-      double2 e[U];
-      double e2[U];
-      double x[U];
-      int iis[U], jjs[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t v = vb + u;
-        iis[u] = -1;
-        jjs[u] = jj;
-        e[u] = make_double2(0.0, 0.0);
-        e2[u] = 0.0;
-        x[u] = 0.0;
-        if (v < v1) {
-          iis[u] = ii;
-          const int64_t r = L.idx[ii], c = L.idx[jj];
-          e[u] = pairs[r + c * n];                              // corr(idx[ii], idx[jj]), net(idx[ii], idx[jj])
-          e2[u] = P.symmetric ? e[u].y : pairs[c + r * n].y;    // net(idx[jj], idx[ii])
-          x[u] = P.disc_cv ? P.disc_cv[cvo + v] : nr_nan();
-          if (++ii == k) {
-            ++jj;
-            ii = jj + 1;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (iis[u] >= 0) {
-          const int i = iis[u], j = jjs[u];
-          if (j != jj64) {  // the chunk crossed into column j: flush the previous column
-            const int jp = (int)jj64;
-            atomicAdd(&plain_w[jp], cpl);
-            if (gj != WD_NO_GRID) {
-              atomicAdd(&L.pb[jp], cpb);
-              atomicAdd(&L.on[jp], con);
-              atomicAdd(&L.tn[jp], ctn);
-              atomicAdd(&L.ff[jp], cff);
-            }
-            cpl = cff = 0.0;
-            cpb = con = ctn = 0;
-            jj64 = j;
-            pj = L.rk[j];
-            gj = L.ge[j];
-          }
-          const double y = e[u].x;
-          if (P.cv_out) P.cv_out[cvo + vb + u] = y;
-          const int pi = L.rk[i];
-          // target jj (column idx[jj]) gains row idx[ii]: registers
-          const double a = fabs(e[u].y);
-          cpl += a;
-          if (gj != WD_NO_GRID && isfinite(a)) {
-            if (((pj ^ pi) & 1) == 0) {
-              if (pi < pj) cpb += wd_fx(a, gj, WD_FX_BITS);
-              else if (pi == pj + 2) cff += a;
-              else ctn += wd_fx(a, gj, 0);
-            } else {
-              con += wd_fx(a, gj, WD_FX_BITS);
-            }
-          }
-          // target ii (column idx[ii]) gains row idx[jj]: LDS
-          wd_add(L, plain_w, i, pi, pj, fabs(e2[u]));
-          const double xv = x[u];
-          if (isfinite(xv) && isfinite(y)) {        // CompleteCases src/netStats.cpp:43-61
-            const double dx = xv - xs, dy = y - ys;
-            acc[0] += 1.0;
-            acc[1] += dx;
-            acc[2] += dy;
-            acc[3] += dx * dx;
-            acc[4] += dy * dy;
-            acc[5] += dx * dy;
-            acc[6] += (xv > 0.0 ? y : (xv < 0.0 ? -y : 0.0));
-          }
-        }
-      }
+  const int64_t nchunks = (npairs + U - 1) / U;
+  if (P.cv_out) {  // vector runs (one item per module): CorrVector out, no pipeline
+    for (int64_t ch = tid; ch < nchunks; ch += BS) {
+      NetChunk<U> c;
+      net_issue<U, SYM>(P, L, k, cvo, npairs, ch, c);
+      net_process<U, true>(P, L, plain_w, cvo, xs, ys, c, acc);
     }
-    {  // flush the last column of the chunk
-      const int jp = (int)jj64;
-      atomicAdd(&plain_w[jp], cpl);
-      if (gj != WD_NO_GRID) {
-        atomicAdd(&L.pb[jp], cpb);
-        atomicAdd(&L.on[jp], con);
-        atomicAdd(&L.tn[jp], ctn);
-        atomicAdd(&L.ff[jp], cff);
-      }
+  } else if (!PIPE) {
+    for (int64_t ch = tid; ch < nchunks; ch += BS) {
+      NetChunk<U> c;
+      net_issue<U, SYM>(P, L, k, cvo, npairs, ch, c);
+      net_process<U, false>(P, L, plain_w, cvo, xs, ys, c, acc);
+    }
+  } else if (tid < nchunks) {
+    // (no global stores in this loop: pending stores next to the gathers
+    // would make every wait a full drain)
+    // two chunks in registers, roles alternating (no register copies, which
+    // would wait for the younger gathers); the issue past the last chunk
+    // re-reads the last chunk and is never processed
+    NetChunk<U> a, b;
+    const int64_t last = nchunks - 1;
+    int64_t ch = tid;
+    net_issue<U, SYM>(P, L, k, cvo, npairs, ch, a);
+    for (;;) {
+      net_issue<U, SYM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
+      net_process<U, false>(P, L, plain_w, cvo, xs, ys, a, acc);
+      ch += BS;
+      if (ch >= nchunks) break;
+      net_issue<U, SYM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
+      net_process<U, false>(P, L, plain_w, cvo, xs, ys, b, acc);
+      ch += BS;
+      if (ch >= nchunks) break;
     }
   }
   block_sums<7, NW>(acc, L.red);   // its barriers also complete the weighted-degree parts
@@ -367,7 +427,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
 // large for LDS at all -- a persistent grid whose workgroups keep the per-node
 // arrays in their global scratch slot (L2-resident; the atomics go to L2) and
 // loop over the items.
-template <int NW, bool BIG>
+template <int NW, bool BIG, bool SYM>
 __global__ void __launch_bounds__(NW * 64)
 module_net_kernel(NetParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -384,7 +444,7 @@ module_net_kernel(NetParams P) {
     if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
     for (int64_t c = threadIdx.x; c < k; c += NW * 64) L.idx[c] = node_index(P.src, key, p_local, off + c);
     __syncthreads();
-    net_item<NW>(P, m, p_local, off, k, L);
+    net_item<NW, NW == 2 || BIG, SYM>(P, m, p_local, off, k, L);
   }
 }
 
@@ -1552,11 +1612,14 @@ hipError_t launch_net(const NetParams& P0, int64_t n_items, hipStream_t st) {
   if (net_kernel_big(P.k_max)) {
     if (!P.big_scratch || P.big_slots <= 0) return hipErrorInvalidValue;
     const unsigned g = (unsigned)(n_items < P.big_slots ? n_items : P.big_slots);
-    hipLaunchKernelGGL((module_net_kernel<4, true>), dim3(g), dim3(256), lds, st, P);
+    if (P.symmetric) hipLaunchKernelGGL((module_net_kernel<4, true, true>), dim3(g), dim3(256), lds, st, P);
+    else hipLaunchKernelGGL((module_net_kernel<4, true, false>), dim3(g), dim3(256), lds, st, P);
   } else if (net_kernel_waves(P.k_max) == 4) {
-    hipLaunchKernelGGL((module_net_kernel<4, false>), dim3((unsigned)n_items), dim3(256), lds, st, P);
+    if (P.symmetric) hipLaunchKernelGGL((module_net_kernel<4, false, true>), dim3((unsigned)n_items), dim3(256), lds, st, P);
+    else hipLaunchKernelGGL((module_net_kernel<4, false, false>), dim3((unsigned)n_items), dim3(256), lds, st, P);
   } else {
-    hipLaunchKernelGGL((module_net_kernel<2, false>), dim3((unsigned)n_items), dim3(128), lds, st, P);
+    if (P.symmetric) hipLaunchKernelGGL((module_net_kernel<2, false, true>), dim3((unsigned)n_items), dim3(128), lds, st, P);
+    else hipLaunchKernelGGL((module_net_kernel<2, false, false>), dim3((unsigned)n_items), dim3(128), lds, st, P);
   }
   return hipGetLastError();
 }

@@ -169,6 +169,16 @@ class Engine:
         self._check(self._lib.nr_observed(self._h, _ptr(out)))
         return out
 
+    def observed_async(self):
+        """Enqueue the observed statistics on the context's second stream
+        (nr_observed_async); collect them with observed_wait()."""
+        self._check(self._lib.nr_observed_async(self._h))
+
+    def observed_wait(self) -> np.ndarray:
+        out = np.empty((self.n_rows, self.n_stat), dtype=np.float64, order="F")
+        self._check(self._lib.nr_observed_wait(self._h, _ptr(out)))
+        return out
+
     def run(self, perm_begin: int, perm_end: int, seed: int = 0, pi=None) -> np.ndarray:
         n = perm_end - perm_begin
         out = np.empty((self.n_rows, self.n_stat, n), dtype=np.float64, order="F")

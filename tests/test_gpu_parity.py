@@ -241,6 +241,29 @@ def test_batching_and_sharding_are_bitwise_invariant():
     assert d == t == 7
 
 
+def test_observed_async_beside_run():
+    """nr_observed_async runs the observed statistics on the context's second
+    stream beside the permutation batches (two batches in flight on the
+    first): both results are bitwise those of the serial calls, and a pending
+    result is dropped by a change of null pool."""
+    lay, mi, disc, tx, tc, tn = _engine_case()
+    eng = _engine_from(mi, disc, tx, tc, tn)
+    obs = eng.observed()
+    eng.set_batch(5)
+    serial = eng.run(0, 24, 5)
+    eng.observed_async()
+    nulls = eng.run(0, 24, 5)
+    got = eng.observed_wait()
+    np.testing.assert_array_equal(got.view(np.uint64), obs.view(np.uint64))
+    np.testing.assert_array_equal(nulls.view(np.uint64), serial.view(np.uint64))
+    with pytest.raises(N.NetRepError):
+        eng.observed_wait()            # nothing pending any more
+    eng.observed_async()
+    eng.set_null_pool(np.arange(eng.shape()[0], dtype=np.int32))
+    with pytest.raises(N.NetRepError):
+        eng.observed_wait()            # dropped by the new null pool
+
+
 def test_lanczos_path_vs_oracle():
     """The one Lanczos path -- start G e_c* (kernels.hip start_column), fp32
     matvecs once the residual drops below 1e-7 theta, the Ritz vector's G v
