@@ -232,9 +232,20 @@ def roofline_terms(sizes, n_samples, with_data):
     return net_bytes, prof_bytes, prof_flops
 
 
+def table_bytes(sizes):
+    """Algorithmic bytes per permutation of the Gram-table profile kernel:
+    one 32-byte table element per pair and per diagonal entry, the column
+    sums, the node indices and the discovery correlations (the data block is
+    not read: the Gram comes from the table)."""
+    k = np.asarray(sizes, dtype=np.float64)
+    return (4 * k + 8 * k * (k - 1) / 2 + 32 * k * (k + 1) / 2 + 8 * k).sum()
+
+
 # Random 16-byte gathers over a 6.4 GB matrix on MI355X (tools/probes/gather_probe.hip,
 # profiles/r02/gather_probe.txt): the line rate the network kernel is bound by.
 GATHER_CEILING_GREADS = 50.0
+# the same probe over the C5 footprint (40,000 nodes, 25.6 GB): profiles/r03/c2c5/gather_probe_40k.txt
+GATHER_CEILING_C5_GREADS = 48.4
 
 
 def gather_ceiling(sizes, perms, seconds):
@@ -471,6 +482,23 @@ def run_c5(args, world, rank, local):
     mk = line["kernels"]["module_profile_kernel"]
     if mk["achieved"] is not None:
         mk["frac"] = mk["achieved"] / mk["peak"]
+    nk = line["kernels"]["module_net_kernel"]
+    if ms0 > 0:
+        nk["gather_ceiling"] = gather_ceiling(sizes, P / max(l0, 1), ms0 / max(l0, 1) / 1e3)
+        nk["gather_ceiling"]["peak_c5_footprint"] = GATHER_CEILING_C5_GREADS
+        nk["gather_ceiling"]["frac_c5_footprint"] = nk["gather_ceiling"]["achieved"] / GATHER_CEILING_C5_GREADS
+    # the dominant kernel (the summary-profile launches of one batch)
+    b_launch = int(round(P / max(l1, 1)))
+    if mk["achieved"] is not None:
+        line["roofline"] = {"kernel": "module_profile_kernel", "bound": "mfma", "achieved": round(mk["achieved"], 4),
+                            "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(mk["frac"], 6),
+                            "traffic": measured_traffic("C5", b_launch, "module_profile_kernel"),
+                            "traffic_unit": "L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 "
+                                            "+ WRITE_SIZE, profiles/pmc_traffic.json)",
+                            "algorithmic_bytes": round(prof_b * b_launch), "launch_permutations": b_launch,
+                            "executed": measured_mfma("C5", b_launch, "module_profile_kernel", ms1 / max(l1, 1))}
+    line["cpu_baseline"] = None
+    line["cpu_baseline_note"] = "the default bench line (C3) carries the CPU baseline"
     print(json.dumps(line))
 
 
@@ -549,7 +577,23 @@ def main():
                 "bound": "hbm", "avg_ms": ms0 / l0, "launches": l0,
                 "achieved": net_b * B / (ms0 / l0 / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "gather_ceiling": gather_ceiling(lay.module_sizes, B, ms0 / l0 / 1e3)}
-        if meta["with_data"]:
+        table = meta["with_data"] and eng.gram_table()
+        if table:
+            # Gram table: network statistics and the packed Gram from one
+            # 32-byte gather per pair; no per-item matrix-core Gram
+            t1 = ms1 / max(l1, 1) / 1e3
+            tab_b = table_bytes(lay.module_sizes)
+            kernels["module_profile_kernel"] = {
+                "bound": "hbm", "avg_ms": ms1 / max(l1, 1), "launches": l1,
+                "achieved": tab_b * B / t1 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "gram_table": True, "fused_network_statistics": fused,
+                "gather_ceiling": gather_ceiling(lay.module_sizes, B, t1),
+                "equivalent_mfma": {
+                    "achieved": prof_f * B / t1 / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": prof_f * B / t1 / 1e12 / FP64_MFMA_PEAK_TFS,
+                    "note": "the per-item Gram flops (2 S k^2) of the matrix-core path over this launch time; "
+                            "with the table they are not executed (the table's one-off X^T X is 2 S n^2)"}}
+        elif meta["with_data"]:
             t1 = ms1 / max(l1, 1) / 1e3
             kernels["module_profile_kernel"] = {
                 "bound": "mfma", "avg_ms": ms1 / max(l1, 1), "launches": l1,
@@ -566,8 +610,14 @@ def main():
                     "traffic": measured_traffic(args.config, B, dom_name),
                     "traffic_unit": "L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 "
                                     "+ WRITE_SIZE, profiles/pmc_traffic.json)",
-                    "algorithmic_bytes": round(((net_b if fused or dom_name == "module_net_kernel" else 0.0)
+                    "algorithmic_bytes": round(table_bytes(lay.module_sizes) * B if table and
+                                               dom_name == "module_profile_kernel" else
+                                               ((net_b if fused or dom_name == "module_net_kernel" else 0.0)
                                                 + (prof_b if dom_name == "module_profile_kernel" else 0.0)) * B)}
+        if table and dom_name == "module_profile_kernel":
+            roofline["gram_table"] = True
+            roofline["gather_ceiling"] = dom["gather_ceiling"]
+            roofline["equivalent_mfma"] = dom["equivalent_mfma"]
         if dom["unit"] == "TFLOP/s":  # executed MFMA flops next to the algorithmic figure (PMC pass)
             roofline["executed"] = measured_mfma(args.config, B, dom_name, dom.get("avg_ms", 0.0))
         cpu = None

@@ -86,6 +86,13 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src);
 
 /* 1 if corr and net of the resident dataset are exactly symmetric. */
 int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric);
+
+/* 1 when the resident dataset carries the Gram table (the data block's
+ * X^T X interleaved with the matrices, built by the first run or observed
+ * call whose modules are mostly packed-class items with k <= S; DESIGN.md
+ * "Gram table"), else 0. */
+int nr_gram_table(nr_ctx* ctx, int* on);
+
 /* CheckFinite (src/checkFinite.cpp:21-28) of the resident corr and net,
  * computed by nr_set_dataset's symmetry pass over the uploaded matrices (no
  * extra scan): 1 = every element finite. The caller raises the reference's

@@ -44,11 +44,15 @@ struct nr_ctx {
 
   // resident dataset
   double2* d_pairs = nullptr;
+  int32_t pairs_es = 1;          // d_pairs element stride in double2: 2 = the Gram table layout
+  double* d_colsum = nullptr;    // [n_nodes] column sums of the data (Gram table)
+  int64_t table_checked = -1;    // modules_serial the Gram-table decision was made for
   double* d_data = nullptr;
   int64_t n_nodes = 0, n_samples = 0;
   std::vector<std::string> node_names;  // column names of a dataset loaded from files
   int64_t data_gen = 0;                 // bumped by every dataset change (reset_dataset)
   int64_t modules_gen = -1;             // data_gen the modules were validated against
+  int64_t modules_serial = 0;           // bumped by every nr_set_modules
   int64_t null_gen = -1;                // data_gen the null pool was validated against
   int symmetric = 0;
   int corr_finite = 0, net_finite = 0;  // CheckFinite of the resident matrices
@@ -216,6 +220,9 @@ void reset_dataset(nr_ctx* ctx) {
   sync_obs(ctx);
   dfree(ctx->d_pairs);
   dfree(ctx->d_data);
+  dfree(ctx->d_colsum);
+  ctx->pairs_es = 1;
+  ctx->table_checked = -1;
   ctx->node_names.clear();
   ctx->n_nodes = 0;
   ctx->n_samples = 0;
@@ -379,7 +386,8 @@ Lane obs_lane(nr_ctx* ctx) {
 // module on the layout of the largest one: at C5 the small modules ran on the
 // one-workgroup-per-CU full-Gram kernel too.)
 int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
-                    const std::vector<int32_t>& k_sorted, int64_t n_perm, const Lane& ln) {
+                    const std::vector<int32_t>& k_sorted, int64_t n_perm, const Lane& ln,
+                    const nr::NetParams* table_np = nullptr, int* fused_from = nullptr) {
   const hipStream_t st = ln.st;
   const int n_mod = (int)k_sorted.size();
   int n_big = 0;
@@ -417,6 +425,15 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.part_global = plan.variant == 4 ? 1 : 0;
     pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples);
     pp.g32_off = plan.g32_off;
+    // Gram table: the packed class (compile-time layout, no dual items) takes
+    // its network statistics and Gram from the table's gathers
+    pp.fused = table_np && plan.variant == 2 && k_max <= nr::kPackedLayoutK && k_max <= pp.n_samples &&
+               nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160));
+    if (pp.fused) {
+      pp.net = *table_np;
+      pp.net.mod_order = pp.mod_order;
+      if (fused_from) *fused_from = seg[i].first;
+    }
     NR_HIP(ctx, hipMemsetAsync(pp.queue, 0, sizeof(int), st));
     NR_HIP(ctx, nr::launch_profile(pp, plan.slots, plan.variant, plan.per_cu, st));
   }
@@ -514,6 +531,8 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
 
   nr::NetParams np{};
   np.pairs = ctx->d_pairs;
+  np.es = ctx->pairs_es;
+  np.colsum = ctx->d_colsum;
   np.n_nodes = ctx->n_nodes;
   np.symmetric = ctx->symmetric;
   np.src = src;
@@ -535,12 +554,22 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   np.slot_avg_cor = data ? 5 : 3;
   np.out = d_out;
   // The network statistics are their own launch (module_net_kernel) ahead of
-  // the summary-profile launches, on the same stream. (Round 2 measured the
-  // network phase fused into the profile items at +0.7%, within run-to-run
-  // noise, and on a concurrent stream at -11%: profiles/r02/profile_variants.txt.)
-  if (ln.timed) timer_begin(ctx, 0, ln.st);
-  if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ctx->order_k_h, n_perm, ln))) return rc;
-  if (ln.timed) timer_end(ctx, 0, n_items, ln.st);
+  // the summary-profile launches, on the same stream -- except with the Gram
+  // table, where the packed profile launch computes them for its modules
+  // from the same gathers that fill its Gram (launch_profiles reports from
+  // which module on, in size order, it did). (Round 2 measured the network
+  // phase fused into the profile items without the table at +0.7%, within
+  // run-to-run noise, and on a concurrent stream at -11%.)
+  const bool table = data && ctx->pairs_es == 2;
+  auto nets = [&](int n_mod) -> int {
+    if (n_mod <= 0) return NR_OK;
+    std::vector<int32_t> ks(ctx->order_k_h.begin(), ctx->order_k_h.begin() + n_mod);
+    if (ln.timed) timer_begin(ctx, 0, ln.st);
+    if (int r2 = launch_nets(ctx, np, ctx->d_mod_order, ks, n_perm, ln)) return r2;
+    if (ln.timed) timer_end(ctx, 0, (int64_t)n_mod * n_perm, ln.st);
+    return NR_OK;
+  };
+  if (!table && (rc = nets(ctx->n_present))) return rc;
 
   if (data) {
     nr::ProfileParams pp{};
@@ -561,12 +590,76 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.queue = ln.counters;
     pp.diag = ln.counters + 1;
     pp.stamps = ln.timed ? ctx->d_stamps : nullptr;
+    int fused_from = ctx->n_present;
     if (ln.timed) timer_begin(ctx, 1, ln.st);
-    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ln);
+    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ln, table ? &np : nullptr,
+                         &fused_from);
     if (rc) return rc;
     if (ln.timed) timer_end(ctx, 1, n_items, ln.st);
+    if (table && (rc = nets(fused_from))) return rc;
   }
   if (ln.timed) timer_collect(ctx);
+  return NR_OK;
+}
+
+// The Gram table ("Gram table"): the data block's whole Gram
+// X^T X (2 S n^2 flops on the matrix cores, once per dataset) interleaved
+// with {corr, net} as {corr, net}, {gram, net^T} per element, so that a packed
+// profile item reads its network values and its Gram entries in one 32-byte
+// gather per pair instead of a separate network launch plus a per-item
+// matrix-core Gram. Built when most of the present modules' summary-profile
+// work is such items (k <= 320, none above S) and the device has the room
+// (40 bytes per matrix element beside the resident pairs during the build).
+int maybe_build_table(nr_ctx* ctx) {
+  if (ctx->table_checked == ctx->modules_serial) return NR_OK;
+  ctx->table_checked = ctx->modules_serial;
+  if (ctx->pairs_es == 2 || !ctx->d_data || ctx->n_present == 0) return NR_OK;
+  const int64_t S = ctx->n_samples, n = ctx->n_nodes;
+  double packed_w = 0.0, total_w = 0.0;
+  int32_t packed_max = 0;
+  for (const int32_t k : ctx->order_k_h) {
+    const double kd = (double)k, Sd = (double)S;
+    const double w = k <= S ? Sd * kd * kd : kd * Sd * Sd;  // the Gram's flops / 2
+    total_w += w;
+    if (k <= nr::kPackedLayoutK) {
+      packed_w += w;
+      packed_max = std::max(packed_max, k);
+    }
+  }
+  if (packed_max > S || packed_w < 0.5 * total_w) return NR_OK;
+  size_t free_b = 0, total_b = 0;
+  NR_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+  const size_t nn = (size_t)n * (size_t)n;
+  if (free_b < nn * 40 + ((size_t)1 << 30)) return NR_OK;
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->obs_stream) NR_HIP(ctx, hipStreamSynchronize(ctx->obs_stream));
+  double* gram = nullptr;
+  double2* tab = nullptr;
+  double* cs = nullptr;
+  auto drop = [&]() {
+    dfree(gram);
+    dfree(tab);
+    dfree(cs);
+  };
+  if (hipMalloc((void**)&gram, nn * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&tab, 2 * nn * sizeof(double2)) != hipSuccess ||
+      hipMalloc((void**)&cs, (size_t)n * sizeof(double)) != hipSuccess) {
+    drop();
+    (void)hipGetLastError();  // no room after all: the per-item Gram path
+    return NR_OK;
+  }
+  hipError_t e = nr::launch_gram_full(ctx->d_data, S, n, gram, cs, ctx->stream);
+  if (e == hipSuccess) e = nr::launch_widen_pairs(ctx->d_pairs, gram, tab, n, ctx->symmetric, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    drop();
+    return hip_fail(ctx, e, "Gram table");
+  }
+  dfree(gram);
+  dfree(ctx->d_pairs);
+  ctx->d_pairs = tab;
+  ctx->d_colsum = cs;
+  ctx->pairs_es = 2;
   return NR_OK;
 }
 
@@ -646,6 +739,7 @@ int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* p
              double* nulls, bool nulls_on_device) {
   int rc = check_ready(ctx, true);
   if (rc) return rc;
+  if ((rc = maybe_build_table(ctx))) return rc;
   if (e < b) return fail(ctx, NR_ERR_INVALID, "perm_end < perm_begin");
   const int n_stat = n_stat_of(ctx);
   const int64_t slice = (int64_t)ctx->n_rows * n_stat;
@@ -795,6 +889,7 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   sync_obs(ctx);
   dfree(ctx->d_pairs);
   dfree(ctx->d_data);
+  dfree(ctx->d_colsum);
   dfree(ctx->d_row_of);
   dfree(ctx->d_node_off);
   dfree(ctx->d_cv_off);
@@ -1128,8 +1223,9 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   NR_HIP(dst, hipSetDevice(dst->device));
   NR_HIP(dst, hipStreamSynchronize(dst->stream));
   reset_dataset(dst);  // on a failure below dst is left with no dataset
-  const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2);
+  const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2) * (size_t)src->pairs_es;
   NR_HIP(dst, hipMalloc((void**)&dst->d_pairs, pair_bytes));
+  if (src->d_colsum) NR_HIP(dst, hipMalloc((void**)&dst->d_colsum, (size_t)src->n_nodes * sizeof(double)));
   const size_t data_bytes = (size_t)(src->n_samples * (src->n_nodes + 2)) * sizeof(double);  // + virtual columns
   if (src->d_data) NR_HIP(dst, hipMalloc((void**)&dst->d_data, data_bytes));
   // Device to device: over xGMI between GPUs, an on-device copy when both
@@ -1137,7 +1233,11 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   NR_HIP(dst, hipMemcpyPeerAsync(dst->d_pairs, dst->device, src->d_pairs, src->device, pair_bytes, dst->stream));
   if (src->d_data)
     NR_HIP(dst, hipMemcpyPeerAsync(dst->d_data, dst->device, src->d_data, src->device, data_bytes, dst->stream));
+  if (src->d_colsum)
+    NR_HIP(dst, hipMemcpyPeerAsync(dst->d_colsum, dst->device, src->d_colsum, src->device,
+                                   (size_t)src->n_nodes * sizeof(double), dst->stream));
   NR_HIP(dst, hipStreamSynchronize(dst->stream));
+  dst->pairs_es = src->pairs_es;
   dst->n_nodes = src->n_nodes;
   dst->n_samples = src->n_samples;
   dst->node_names = src->node_names;
@@ -1151,6 +1251,12 @@ int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric) {
   if (!ctx || !symmetric) return NR_ERR_INVALID;
   if (!ctx->d_pairs) return fail(ctx, NR_ERR_INVALID, "no dataset");
   *symmetric = ctx->symmetric;
+  return NR_OK;
+}
+
+int nr_gram_table(nr_ctx* ctx, int* on) {
+  if (!ctx || !on) return NR_ERR_INVALID;
+  *on = ctx->d_pairs && ctx->pairs_es == 2 ? 1 : 0;
   return NR_OK;
 }
 
@@ -1174,6 +1280,7 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   sync_obs(ctx);
   ctx->modules_gen = -1;  // usable only once everything below has succeeded
+  ++ctx->modules_serial;
   ctx->n_rows = n_rows;
   ctx->n_present = n_present;
   ctx->node_off_h.assign(node_off, node_off + (n_present > 0 ? n_present + 1 : 0));
@@ -1258,6 +1365,7 @@ int nr_observed(nr_ctx* ctx, double* observed) {
   const int64_t slice = (int64_t)ctx->n_rows * n_stat_of(ctx);
   rc = ensure(ctx, ctx->d_out, ctx->out_cap, (size_t)slice);
   if (rc) return rc;
+  if ((rc = maybe_build_table(ctx))) return rc;
   const nr::IndexSource src = make_source(ctx, nr::NR_IDX_DIRECT, 0, 0, nullptr, ctx->d_test_idx);
   rc = launch_batch(ctx, src, 1, ctx->d_out, main_lane(ctx));
   if (rc) return rc;
@@ -1278,6 +1386,7 @@ int nr_observed_async(nr_ctx* ctx) {
     NR_HIP(ctx, hipMemset(ctx->obs_counters, 0, 16 * sizeof(int)));
   }
   sync_obs(ctx);  // a previous observed launch is done before its buffers are reused
+  if ((rc = maybe_build_table(ctx))) return rc;
   const int64_t slice = (int64_t)ctx->n_rows * n_stat_of(ctx);
   rc = ensure(ctx, ctx->d_obs, ctx->obs_cap, (size_t)std::max<int64_t>(slice, 1));
   if (rc) return rc;
@@ -1387,6 +1496,8 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
     nr::IndexSource src = make_source(ctx, nr::NR_IDX_DIRECT, 0, 0, nullptr, d_idx);
     nr::NetParams np{};
     np.pairs = ctx->d_pairs;
+    np.es = ctx->pairs_es;
+    np.colsum = ctx->d_colsum;
     np.n_nodes = ctx->n_nodes;
     np.symmetric = ctx->symmetric;
     np.src = src;

@@ -23,7 +23,10 @@ struct IndexSource {
 };
 
 struct NetParams {
-  const double2* pairs;        // interleaved {corr, net}, column-major n x n
+  const double2* pairs;        // interleaved {corr, net}, column-major n x n (es = 1), or the
+                               // Gram table: {corr, net}, {gram, net^T} per (i, j) (es = 2)
+  int32_t es;                  // element stride of pairs in double2 units (1 or 2)
+  const double* colsum;        // [n_nodes] column sums of the data (Gram table only)
   int64_t n_nodes;
   int symmetric;               // both matrices exactly symmetric
   IndexSource src;
@@ -85,6 +88,11 @@ struct ProfileParams {
   int32_t order_tail;          // queue order: 0 = module-major (large modules first); T > 0 =
                                // permutation-major over all modules (a size mix in flight) for the
                                // first n_perm - T permutations, the last T module-major
+  // Gram table (packed kernel only): the network statistics of each item are
+  // computed in the profile workgroup from one gather per pair of the table,
+  // which also fills the item's packed Gram (no matrix-core Gram for k <= S)
+  int32_t fused;
+  NetParams net;
 };
 
 size_t net_kernel_lds(int k_max);
@@ -95,6 +103,17 @@ size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant);
 int64_t packed_gram_doubles(int kc);
 int profile_kvec_max(int m_max);  // longest LDS vectors of the large-module layout (variant 4)
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
+// Whether the packed kernel's LDS (vectors of kvec, basis mmax) holds the
+// network item's per-node arrays (the fused Gram-table path).
+bool fused_net_fits(int kvec, int mmax);
+// The Gram table of a dataset with data: gram[i + j n] = x_i . x_j over the
+// n_samples rows of X (n_samples x (n + 2), the virtual columns behind), and
+// colsum[j] = sum of column j.
+hipError_t launch_gram_full(const double* X, int64_t S, int64_t n, double* gram, double* colsum, hipStream_t st);
+// {corr, net} pairs (es = 1) + gram -> the table layout (es = 2):
+// out[2e] = in[e], out[2e + 1] = {gram[e], net(j, i)} for e = i + j n.
+hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* out, int64_t n, int symmetric,
+                              hipStream_t st);
 // variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);

@@ -179,10 +179,36 @@ __device__ __forceinline__ double wd_final(const NetLds& L, int NWn, int c, int 
 // a global (not constant) cell, so the discovery-load pointer stays a global pointer
 __device__ double kNetNanCell = __builtin_nan("");
 
+// The packed symmetric Gram's addressing (layout described at
+// packed_gram_doubles below).
+__host__ __device__ __forceinline__ int pk_pad(int kc) { return (kc + 15) & ~15; }
+__host__ __device__ __forceinline__ int64_t pk_base(int g, int P) {
+  return 16 * (int64_t)g * P - 128 * (int64_t)g * (g - 1);
+}
+__device__ __forceinline__ int64_t pk_at(int r, int c, int kc) {  // r >= 16 (c / 16)
+  const int P = pk_pad(kc);
+  const int g = c >> 4;
+  const int rr = r - 16 * g;
+  const int j = rr >> 6;
+  const int h = min(64, P - 16 * g - 64 * j);
+  return pk_base(g, P) + 1024 * (int64_t)j + (int64_t)(c & 15) * h + (rr & 63);
+}
+__device__ __forceinline__ int64_t pk_col(int c, int kc) { return pk_at(c, c, kc); }  // the diagonal G_cc
+
+// Where a Gram-table item puts its Gram: the slot's packed Gram (and its fp32
+// copy) of side kc = k + 1, the ones column's entries from colsum, and S.
+struct GramOut {
+  double* G;
+  float* G32;
+  int kc;
+  double S;
+};
+
 template <int U>
 struct NetChunk {
   double2 e[U];   // {corr, net}(idx[ii], idx[jj])
   double e2[U];   // net(idx[jj], idx[ii])
+  double g[U];    // gram(idx[ii], idx[jj]) (Gram table)
   double x[U];    // the discovery correlation of the pair
   int iis[U];     // row node (-1: past the end)
   int jjs[U];     // column node
@@ -190,16 +216,19 @@ struct NetChunk {
   int j0;         // its column
 };
 
-// Every lane issues all U (2U when the network is not symmetric) gathers and
-// U discovery loads whatever its chunk holds -- entries past the item's end
-// read the item's first diagonal pair and first discovery value -- so the
-// number of loads in flight is the same on every path and the compiler's
-// wait counts can leave the next chunk's gathers outstanding (PIPE).
-template <int U, bool SYM>
+// Every lane issues all U (2U when the network is not symmetric or the Gram
+// table is read) gathers and U discovery loads whatever its chunk holds --
+// entries past the item's end read the item's first diagonal pair and first
+// discovery value -- so the number of loads in flight is the same on every
+// path and the compiler's wait counts can leave the next chunk's gathers
+// outstanding (PIPE). Table layout (es = 2): the pair's second 16 bytes,
+// {gram, net^T}, sit in the same 32-byte sector as {corr, net}.
+template <int U, bool SYM, bool GRAM>
 __device__ __forceinline__ void net_issue(const NetParams& P, const NetLds& L, int64_t k, int64_t cvo,
                                           int64_t npairs, int64_t ch, NetChunk<U>& c) {
   const double2* __restrict__ pairs = P.pairs;
   const int64_t n = P.n_nodes;
+  const int64_t es = P.es;
   const int64_t v0 = ch * U;
   const int64_t v1 = v0 + U < npairs ? v0 + U : npairs;
   // no discovery vector (observed / vector runs): every x reads the NaN cell
@@ -217,8 +246,17 @@ __device__ __forceinline__ void net_issue(const NetParams& P, const NetLds& L, i
     c.iis[u] = ok ? ii : -1;
     c.jjs[u] = jj;
     const int64_t r = L.idx[ok ? ii : 0], cc = L.idx[ok ? jj : 0];
-    c.e[u] = pairs[r + cc * n];                 // corr(idx[ii], idx[jj]), net(idx[ii], idx[jj])
-    c.e2[u] = SYM ? c.e[u].y : pairs[cc + r * n].y;   // net(idx[jj], idx[ii])
+    const int64_t a = (r + cc * n) * es;
+    c.e[u] = pairs[a];                          // corr(idx[ii], idx[jj]), net(idx[ii], idx[jj])
+    if (GRAM) {  // (symmetry a run-time select: the load is there either way)
+      const double2 f = pairs[a + 1];           // gram(idx[ii], idx[jj]), net(idx[jj], idx[ii])
+      c.g[u] = f.x;
+      c.e2[u] = P.symmetric ? c.e[u].y : f.y;
+    } else if (SYM) {
+      c.e2[u] = c.e[u].y;
+    } else {                                    // net(idx[jj], idx[ii])
+      c.e2[u] = es == 2 ? pairs[a + 1].y : pairs[cc + r * n].y;
+    }
     c.x[u] = xp[(ok ? v : v0) * xstep];
     if (ok && ++ii == k) {
       ++jj;
@@ -227,9 +265,10 @@ __device__ __forceinline__ void net_issue(const NetParams& P, const NetLds& L, i
   }
 }
 
-template <int U, bool STORE>
+template <int U, bool STORE, bool GRAM>
 __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L, double* plain_w, int64_t cvo,
-                                            double xs, double ys, const NetChunk<U>& c, double* acc) {
+                                            double xs, double ys, const NetChunk<U>& c, double* acc,
+                                            const GramOut& go, double& g1) {
   // the column's parts, in registers until the column changes
   int jc = c.j0;
   int pj = L.rk[jc];
@@ -256,6 +295,13 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
       }
       const double y = c.e[u].x;
       if (STORE) P.cv_out[cvo + c.v0 + u] = y;
+      if (GRAM) {  // G_ij (i > j: the packed lower triangle), twice in 1'G1
+        const double gv = c.g[u];
+        const int64_t at = pk_at(i, j, go.kc);
+        go.G[at] = gv;
+        if (go.G32) go.G32[at] = (float)gv;
+        g1 += 2.0 * gv;
+      }
       const int pi = L.rk[i];
       // target jj (column idx[jj]) gains row idx[ii]: registers
       const double a = fabs(c.e[u].y);
@@ -294,14 +340,22 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
   }
 }
 
-template <int NW, bool PIPE, bool SYM, int U = 7>
+// GRAM (the Gram-table items of the packed profile kernel): the item's packed
+// Gram is filled from the same gathers -- G_ij for every pair, the diagonal and
+// the ones column here -- into a region the caller zeroed; g1 / bad return
+// this thread's part of 1'G1 over the data block and a non-finite-diagonal flag.
+template <int NW, bool PIPE, bool SYM, bool GRAM = false, int U = 7>
 __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_local, int64_t off, int64_t k,
-                                         const NetLds& L) {
+                                         const NetLds& L, const GramOut& go = GramOut{}, double* g1_out = nullptr,
+                                         int* bad_out = nullptr) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const double2* __restrict__ pairs = P.pairs;
   const int64_t n = P.n_nodes;
+  const int64_t es = P.es;
+  double g1 = 0.0;
+  int bad = 0;
   // per node: sorted position (SortNodes, src/netStats.cpp:23-32), |diag|,
   // grid exponent, zeroed accumulators
   for (int64_t c = tid; c < k; c += BS) {
@@ -309,7 +363,21 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     int r = 0;
     for (int64_t c2 = 0; c2 < k; ++c2) r += L.idx[c2] < ic;
     L.rk[c] = r;
-    const double d = fabs(pairs[(int64_t)ic + (int64_t)ic * n].y);
+    const int64_t ad = ((int64_t)ic + (int64_t)ic * n) * es;
+    const double d = fabs(pairs[ad].y);
+    if (GRAM) {  // G_cc and the ones column's G_kc = sum of column c
+      const double gcc = pairs[ad + 1].x;
+      const double cs = P.colsum[ic];
+      const int64_t a1 = pk_at((int)c, (int)c, go.kc), a2 = pk_at((int)k, (int)c, go.kc);
+      go.G[a1] = gcc;
+      go.G[a2] = cs;
+      if (go.G32) {
+        go.G32[a1] = (float)gcc;
+        go.G32[a2] = (float)cs;
+      }
+      g1 += gcc;
+      bad |= (int)!isfinite(gcc);
+    }
     L.dg[c] = d;
     L.ge[c] = wd_grid_exp(d);
 #pragma unroll
@@ -330,22 +398,27 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   // (dropped by CompleteCases, src/netStats.cpp:43-61) falls back to 0 so it
   // cannot poison the other pairs' sums.
   const double xs = P.cv_shift ? P.cv_shift[m] : 0.0;
-  const double y0 = npairs > 0 ? pairs[(int64_t)L.idx[1] + (int64_t)L.idx[0] * n].x : 0.0;
+  const double y0 = npairs > 0 ? pairs[((int64_t)L.idx[1] + (int64_t)L.idx[0] * n) * es].x : 0.0;
+  if (GRAM && tid == 0) {  // 1'1 = S
+    const int64_t a = pk_at((int)k, (int)k, go.kc);
+    go.G[a] = go.S;
+    if (go.G32) go.G32[a] = (float)go.S;
+  }
   const double ys = isfinite(y0) ? y0 : 0.0;
 
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};  // n, sx, sy, sxx, syy, sxy, s(sign(x) y)
   const int64_t nchunks = (npairs + U - 1) / U;
-  if (P.cv_out) {  // vector runs (one item per module): CorrVector out, no pipeline
+  if (!GRAM && P.cv_out) {  // vector runs (one item per module): CorrVector out, no pipeline
     for (int64_t ch = tid; ch < nchunks; ch += BS) {
       NetChunk<U> c;
-      net_issue<U, SYM>(P, L, k, cvo, npairs, ch, c);
-      net_process<U, true>(P, L, plain_w, cvo, xs, ys, c, acc);
+      net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch, c);
+      net_process<U, true, false>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
     }
-  } else if (!PIPE) {
+  } else if (GRAM || !PIPE) {
     for (int64_t ch = tid; ch < nchunks; ch += BS) {
       NetChunk<U> c;
-      net_issue<U, SYM>(P, L, k, cvo, npairs, ch, c);
-      net_process<U, false>(P, L, plain_w, cvo, xs, ys, c, acc);
+      net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch, c);
+      net_process<U, false, GRAM>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
     }
   } else if (tid < nchunks) {
     // (no global stores in this loop: pending stores next to the gathers
@@ -356,14 +429,14 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     NetChunk<U> a, b;
     const int64_t last = nchunks - 1;
     int64_t ch = tid;
-    net_issue<U, SYM>(P, L, k, cvo, npairs, ch, a);
+    net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch, a);
     for (;;) {
-      net_issue<U, SYM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
-      net_process<U, false>(P, L, plain_w, cvo, xs, ys, a, acc);
+      net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
+      net_process<U, false, false>(P, L, plain_w, cvo, xs, ys, a, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
-      net_issue<U, SYM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
-      net_process<U, false>(P, L, plain_w, cvo, xs, ys, b, acc);
+      net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
+      net_process<U, false, false>(P, L, plain_w, cvo, xs, ys, b, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
     }
@@ -418,6 +491,10 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     o[(int64_t)P.n_rows * P.slot_cor_cor] = na_fill(cor_cor);
     o[(int64_t)P.n_rows * P.slot_cor_degree] = na_fill(cor_degree);
     o[(int64_t)P.n_rows * P.slot_avg_cor] = na_fill(avg_cor);
+  }
+  if (GRAM) {
+    *g1_out = g1;
+    *bad_out = bad;
   }
   __syncthreads();  // LDS free again
 }
@@ -580,19 +657,6 @@ __device__ __forceinline__ double reorthogonalise_cgs(const double* __restrict__
 // columns one after the other, h rows each. A matvec unit (group, chunk) is
 // then one contiguous run of 16 h doubles, every column piece starting on a
 // 128-byte line (packed_matvec). Group g starts at pk_base(g, P).
-__host__ __device__ __forceinline__ int pk_pad(int kc) { return (kc + 15) & ~15; }
-__host__ __device__ __forceinline__ int64_t pk_base(int g, int P) {
-  return 16 * (int64_t)g * P - 128 * (int64_t)g * (g - 1);
-}
-__device__ __forceinline__ int64_t pk_at(int r, int c, int kc) {  // r >= 16 (c / 16)
-  const int P = pk_pad(kc);
-  const int g = c >> 4;
-  const int rr = r - 16 * g;
-  const int j = rr >> 6;
-  const int h = min(64, P - 16 * g - 64 * j);
-  return pk_base(g, P) + 1024 * (int64_t)j + (int64_t)(c & 15) * h + (rr & 63);
-}
-__device__ __forceinline__ int64_t pk_col(int c, int kc) { return pk_at(c, c, kc); }  // the diagonal G_cc
 
 // Stores one 16 x 16 MFMA accumulator tile of the Gram's super-tile (I2, J2)
 // into the packed layout: lane (i16, kk) holds rows gj = 32 J2 + 16 b + i16 of
@@ -1403,15 +1467,41 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       Li.q = gnode + 2 * (int64_t)P.k_max;
       Li.w = gnode + 3 * (int64_t)P.k_max;
     }
-    // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     const bool dual = k > S;
     const int n = dual ? S : k;  // Lanczos dimension
     const int kc = n + 1;
     double g1[1] = {0.0};
     int bad = 0;
+    bool gram_done = false;
+    if (PACKED && P.fused && !dual) {
+      // Gram table: the item's network statistics from one 32-byte gather per
+      // pair, which also carries G_ij -- the packed Gram is filled here (into
+      // a zeroed region: padding and the diagonal blocks' upper parts stay 0)
+      // and the matrix-core Gram is skipped. The per-node arrays live in the
+      // Lanczos vectors' LDS, idle until the Lanczos phase.
+      const GramOut go{G, G32, kc, Sd};
+      {
+        const int64_t ng = pk_base(pk_pad(kc) / 16, pk_pad(kc));
+        for (int64_t i = tid; i < ng; i += BS) {
+          G[i] = 0.0;
+          if (G32) G32[i] = 0.0f;
+        }
+        __syncthreads();
+      }
+      // (the engine fuses only launches without dual items: k <= S)
+      const NetLds NL = carve_net_over<NW>(L.q, L.red, L.idx, kmax);
+      double gp = 0.0;
+      int bp = 0;
+      net_item<NW, false, true, true, 7>(P.net, m, p_local, off, k, NL, go, &gp, &bp);
+      g1[0] = gp;
+      bad = bp;
+      gram_done = true;
+      for (int64_t i = tid; i < n_part; i += BS) part[i] = 0.0;  // the per-node arrays overlapped them
+    }
+    // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     if (dual)
       gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
-    else
+    else if (!gram_done)
       gram_mfma<NW, PACKED>(X, S, L.idx, k, P.ones_off, G, G32, ld, g1[0], bad);
     if (bad) atomicOr(&s_flags[1], 1);
     block_sums<1, NW>(g1, L.red);  // barriers also publish G to the whole workgroup
@@ -1481,6 +1571,110 @@ __global__ void interleave_kernel(const double* __restrict__ corr, const double*
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_elem;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = make_double2(corr[i], net[i]);
+}
+
+// Gram table of the resident data block: gram[i + j n] = x_i . x_j (fp64
+// matrix cores, the super-tile scheme of gram_mfma over the whole matrix, one
+// 32 x 32 super-tile per wave; columns past n read the zero column n + 1).
+// Computed once per dataset (2 S n^2 flops) for the Gram-table items.
+__global__ void __launch_bounds__(256)
+gram_full_kernel(const double* __restrict__ X, int S, int64_t n, double* __restrict__ gram) {
+  const int lane = threadIdx.x & 63;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int64_t T = (n + 31) / 32;
+  const int full = S / 16 * 16;
+  const int64_t zero_col = (n + 1) * (int64_t)S;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < T * T; t += (int64_t)gridDim.x * 4) {
+    const int64_t I = t % T, J = t / T;
+    const double* col[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int64_t c = (o < 2 ? I : J) * 32 + (o & 1) * 16 + i16;
+      col[o] = X + (c < n ? c * S : zero_col) + 4 * kk;
+    }
+    nr_f64x4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+    double v[4][4];
+    for (int s0 = 0; s0 < S; s0 += 16) {
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        if (s0 < full) {
+          double2 p0, p1;
+          __builtin_memcpy(&p0, col[o] + s0, sizeof(double2));
+          __builtin_memcpy(&p1, col[o] + s0 + 2, sizeof(double2));
+          v[o][0] = p0.x;
+          v[o][1] = p0.y;
+          v[o][2] = p1.x;
+          v[o][3] = p1.y;
+        } else {  // the last, partial step
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[o][q] = s0 + 4 * kk + q < S ? col[o][s0 + q] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[0][q], v[2][q], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[0][q], v[3][q], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[1][q], v[2][q], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[1][q], v[3][q], acc[1][1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // D[row = (lane>>4) + 4r][col = lane & 15] (f64 MFMA C/D map), as gram_mfma
+          const int64_t gi = I * 32 + 16 * a + kk + 4 * r;
+          const int64_t gj = J * 32 + 16 * b + i16;
+          if (gi < n && gj < n) gram[gi + gj * n] = acc[a][b][r];
+        }
+  }
+}
+
+// colsum[j] = sum over the S rows of column j (one wave per column).
+__global__ void colsum_kernel(const double* __restrict__ X, int S, int64_t n, double* __restrict__ colsum) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t c = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < n;
+       c += (int64_t)gridDim.x * (blockDim.x >> 6)) {
+    double a = 0.0;
+    for (int s = lane; s < S; s += 64) a += X[c * S + s];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (lane == 0) colsum[c] = a;
+  }
+}
+
+// {corr, net} + gram -> the table layout {corr, net}, {gram, net^T} per
+// element, 32 x 32 tiles (net^T staged in LDS so both reads are coalesced).
+__global__ void __launch_bounds__(256)
+widen_pairs_kernel(const double2* __restrict__ in, const double* __restrict__ gram, double2* __restrict__ out,
+                   int64_t n, int symmetric) {
+  __shared__ double t[32][33];
+  const int64_t r0 = (int64_t)blockIdx.x * 32, c0 = (int64_t)blockIdx.y * 32;
+  const int i = threadIdx.x & 31;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = (threadIdx.x >> 5) + 8 * q;
+    // t[j][i] = net(c0 + j, r0 + i)... staged as t[jj][ii] = in[(c0 + ii) + (r0 + jj) n].y
+    if (!symmetric && c0 + i < n && r0 + j < n) t[j][i] = in[(c0 + i) + (r0 + j) * n].y;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = (threadIdx.x >> 5) + 8 * q;
+    const int64_t r = r0 + i, c = c0 + j;
+    if (r < n && c < n) {
+      const int64_t e = r + c * n;
+      const double2 p = in[e];
+      out[2 * e] = p;
+      out[2 * e + 1] = make_double2(gram[e], symmetric ? p.y : t[i][j]);   // net(c, r)
+    }
+  }
 }
 
 // Exact symmetry check of the interleaved matrix via 32x32 LDS tiles: block
@@ -1646,6 +1840,33 @@ hipError_t launch_interleave(const double* corr, const double* net, double2* out
                              hipStream_t st) {
   hipLaunchKernelGGL(interleave_kernel, dim3(4096), dim3(256), 0, st, corr, net, out, n_elem);
   return hipGetLastError();
+}
+
+hipError_t launch_gram_full(const double* X, int64_t S, int64_t n, double* gram, double* colsum, hipStream_t st) {
+  const int64_t T = (n + 31) / 32;
+  const unsigned g = (unsigned)std::min<int64_t>((T * T + 3) / 4, 8192);
+  hipLaunchKernelGGL(gram_full_kernel, dim3(g), dim3(256), 0, st, X, (int)S, n, gram);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)std::min<int64_t>((n + 3) / 4, 4096)), dim3(256), 0, st, X,
+                     (int)S, n, colsum);
+  return hipGetLastError();
+}
+
+hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* out, int64_t n, int symmetric,
+                              hipStream_t st) {
+  const unsigned nb = (unsigned)((n + 31) / 32);
+  hipLaunchKernelGGL(widen_pairs_kernel, dim3(nb, nb), dim3(256), 0, st, in, gram, out, n, symmetric);
+  return hipGetLastError();
+}
+
+bool fused_net_fits(int kvec, int mmax) {
+  // NetLds (carve_net_over, from L.q; its reduction scratch is L.red) against
+  // the LzLds span from q up to idx (carve_lds, twork in the partials)
+  const size_t need = net_lds_bytes(NR_WAVES, kvec) - sizeof(double) * 8 * NR_WAVES;
+  const size_t have = sizeof(double) * (6 * (size_t)kvec + (size_t)packed_part_doubles(NR_WAVES, kvec, mmax) +
+                                        4 * (size_t)mmax + 3 * ((size_t)mmax + 1));
+  return need <= have;
 }
 
 hipError_t launch_symmetry(const double2* a, int64_t n, int* asym, hipStream_t st) {

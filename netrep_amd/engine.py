@@ -169,6 +169,12 @@ class Engine:
         self._check(self._lib.nr_observed(self._h, _ptr(out)))
         return out
 
+    def gram_table(self) -> bool:
+        """Whether the resident dataset carries the Gram table (nr_gram_table)."""
+        on = C.c_int()
+        self._check(self._lib.nr_gram_table(self._h, C.byref(on)))
+        return bool(on.value)
+
     def observed_async(self):
         """Enqueue the observed statistics on the context's second stream
         (nr_observed_async); collect them with observed_wait()."""
