@@ -46,24 +46,26 @@ FP64_MFMA_PEAK_TFS = 78.6    # MI355X fp64 matrix peak (spec)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def measured_traffic(config, batch, kernel):
+def measured_traffic(config, batch, kernel, table=False):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
     (tools/collect_pmc.sh + tools/summarize_pmc.py: FETCH_SIZE x2 gfx950
     correction + WRITE_SIZE, per MI355X_MICROARCH.md). PMC counters cannot be
     read from inside the timed run, so the number is the one measured on the
-    same command; null when no pass matches this config/batch/kernel."""
+    same command; null when no pass matches this config/batch/kernel (and
+    Gram-table mode: the table kernel's passes carry "gram_table": true)."""
     try:
         with open(TRAFFIC_FILE) as f:
             rows = json.load(f)
     except (OSError, ValueError):
         return None
     for r in rows:
-        if r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel:
+        if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
+                and bool(r.get("gram_table", False)) == table):
             return float(r["hbm_bytes_per_launch"])
     return None
 
 
-def measured_mfma(config, batch, kernel, avg_ms):
+def measured_mfma(config, batch, kernel, avg_ms, table=False):
     """Executed fp64 MFMA work of `kernel` from the same committed PMC pass
     (SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 flops per launch, tools/summarize_pmc.py),
     as TFLOP/s over this run's HIP-event launch time, and the MFMA-busy share
@@ -76,7 +78,7 @@ def measured_mfma(config, batch, kernel, avg_ms):
         return None
     for r in rows:
         if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
-                and "mfma_f64_flops_executed" in r and avg_ms > 0):
+                and bool(r.get("gram_table", False)) == table and "mfma_f64_flops_executed" in r and avg_ms > 0):
             return {"executed_TFLOPs": round(r["mfma_f64_flops_executed"] / (avg_ms * 1e-3) / 1e12, 4),
                     "mfma_busy_pct": round(r.get("mfma_busy_pct", float("nan")), 2)}
     return None
@@ -579,20 +581,28 @@ def main():
                 "gather_ceiling": gather_ceiling(lay.module_sizes, B, ms0 / l0 / 1e3)}
         table = meta["with_data"] and eng.gram_table()
         if table:
-            # Gram table: network statistics and the packed Gram from one
-            # 32-byte gather per pair; no per-item matrix-core Gram
+            # Gram table: every statistic of a module-permutation in this one
+            # launch -- network values and the packed Gram from one 32-byte
+            # table gather per pair, then the Lanczos eigenpair. The roofline
+            # keeps SURVEY.md 8d's algorithmic units (Gram flops F(k), bytes
+            # B(k)); the Gram flops are served by the per-dataset table X^T X
+            # (2 S n^2 once) instead of being executed per item.
             t1 = ms1 / max(l1, 1) / 1e3
             tab_b = table_bytes(lay.module_sizes)
             kernels["module_profile_kernel"] = {
-                "bound": "hbm", "avg_ms": ms1 / max(l1, 1), "launches": l1,
-                "achieved": tab_b * B / t1 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "bound": "mfma", "avg_ms": ms1 / max(l1, 1), "launches": l1,
+                "achieved": prof_f * B / t1 / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "gram_table": True, "fused_network_statistics": fused,
-                "gather_ceiling": gather_ceiling(lay.module_sizes, B, t1),
-                "equivalent_mfma": {
-                    "achieved": prof_f * B / t1 / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                    "frac": prof_f * B / t1 / 1e12 / FP64_MFMA_PEAK_TFS,
-                    "note": "the per-item Gram flops (2 S k^2) of the matrix-core path over this launch time; "
-                            "with the table they are not executed (the table's one-off X^T X is 2 S n^2)"}}
+                "units_note": "achieved = SURVEY.md 8d algorithmic Gram flops F(k) = 2 S k min(S,k) per "
+                              "module-permutation / launch time; per item they come from the dataset's Gram "
+                              "table (2 S n^2 flops once per dataset), not from executed MFMA",
+                "hbm": {"achieved": (net_b + prof_b) * B / t1 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": (net_b + prof_b) * B / t1 / 1e9 / HBM_PEAK_GBS,
+                        "note": "SURVEY.md 8d algorithmic bytes B(k) incl. 8 S k data bytes"},
+                "table_gather_bytes": {"achieved": tab_b * B / t1 / 1e9, "unit": "GB/s",
+                                       "note": "32-byte table element per pair and diagonal entry + indices + "
+                                               "discovery vectors, the bytes this kernel's gathers need"},
+                "gather_ceiling": gather_ceiling(lay.module_sizes, B, t1)}
         elif meta["with_data"]:
             t1 = ms1 / max(l1, 1) / 1e3
             kernels["module_profile_kernel"] = {
@@ -607,19 +617,18 @@ def main():
         dom = kernels[dom_name]
         roofline = {"kernel": dom_name, "bound": dom["bound"], "achieved": round(dom["achieved"], 4),
                     "peak": dom["peak"], "unit": dom["unit"], "frac": round(dom["frac"], 6),
-                    "traffic": measured_traffic(args.config, B, dom_name),
+                    "traffic": measured_traffic(args.config, B, dom_name, bool(table)),
                     "traffic_unit": "L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 "
                                     "+ WRITE_SIZE, profiles/pmc_traffic.json)",
-                    "algorithmic_bytes": round(table_bytes(lay.module_sizes) * B if table and
-                                               dom_name == "module_profile_kernel" else
-                                               ((net_b if fused or dom_name == "module_net_kernel" else 0.0)
+                    "algorithmic_bytes": round(((net_b if fused or dom_name == "module_net_kernel" else 0.0)
                                                 + (prof_b if dom_name == "module_profile_kernel" else 0.0)) * B)}
         if table and dom_name == "module_profile_kernel":
             roofline["gram_table"] = True
+            roofline["units_note"] = dom["units_note"]
+            roofline["hbm"] = dom["hbm"]
             roofline["gather_ceiling"] = dom["gather_ceiling"]
-            roofline["equivalent_mfma"] = dom["equivalent_mfma"]
         if dom["unit"] == "TFLOP/s":  # executed MFMA flops next to the algorithmic figure (PMC pass)
-            roofline["executed"] = measured_mfma(args.config, B, dom_name, dom.get("avg_ms", 0.0))
+            roofline["executed"] = measured_mfma(args.config, B, dom_name, dom.get("avg_ms", 0.0), bool(table))
         cpu = None
         if world == 1 and not args.no_cpu_baseline and host is not None:
             rate, dt, n_cpu, threads, hc = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)

@@ -215,9 +215,11 @@ int nr_get_diagnostics(nr_ctx* ctx, int64_t* eig_items, int64_t* eig_steps,
                        int64_t* eig_cap_hits, int64_t* eig_reorths);
 int nr_synchronize(nr_ctx* ctx);
 /* Diagnostics: per-phase shader-cycle stamps of the summary-profile kernel,
- * summed over workgroups (0 index, 1 Gram, 2 Lanczos vector work, 3 Lanczos
- * matvec, 4 reorthogonalisation, 5 tail). Off by default; a run with stamps
- * on is a measurement run, not a timed one. */
+ * summed over workgroups, 16 slots (0 index, 1 Gram, 2 Lanczos set-up,
+ * 3 matvec, 4 three-term step + omega, 5 statistics, 6 q update, 7 Ritz
+ * checks, 8 start column, 9 reorthogonalisation, 10 Ritz vector,
+ * 11 node contributions, 12 Ritz coefficients; 13-15 spare). Off by default; a run with stamps on
+ * is a measurement run, not a timed one. */
 int nr_set_stamps(nr_ctx* ctx, int enable);
 int nr_get_stamps(nr_ctx* ctx, uint64_t* cycles);
 

@@ -147,18 +147,32 @@ static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha,
     const double x = (lo + (hi - lo) * (double)(lane + 1) / den) * inv;
     double p0 = 1.0, p1 = alpha[0] * inv - x;
     int cnt = p1 < 0.0;  // eigenvalues < x
-#pragma unroll 4
-    for (int i = 1; i < n; ++i) {
-      const double b = beta[i - 1] * inv;
-      const double p2 = fma(alpha[i] * inv - x, p1, -(b * b) * p0);
-      cnt += (p2 < 0.0) != (p1 < 0.0);
-      p0 = p1;
-      p1 = p2;
-      if ((i & 3) == 0) {
-        const double mg = fabs(p1);
-        const double s = mg > 1e150 ? 1e-150 : (mg < 1e-150 ? 1e150 : 1.0);
-        p0 *= s;
-        p1 *= s;
+    // 8 steps' alpha/beta read ahead of their recurrence steps, so the LDS
+    // latency is paid once per 8 steps instead of on the dependency chain of
+    // every step (same arithmetic in the same order)
+    for (int i0 = 1; i0 < n; i0 += 8) {
+      double av[8], bv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int i = min(i0 + t, n - 1);
+        av[t] = alpha[i];
+        bv[t] = beta[i - 1];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        if (i0 + t < n) {
+          const double b = bv[t] * inv;
+          const double p2 = fma(av[t] * inv - x, p1, -(b * b) * p0);
+          cnt += (p2 < 0.0) != (p1 < 0.0);
+          p0 = p1;
+          p1 = p2;
+          if ((t & 3) == 3) {  // i = i0 + t with i0 = 1 mod 8: i = 0 mod 4
+            const double mg = fabs(p1);
+            const double s = mg > 1e150 ? 1e-150 : (mg < 1e-150 ? 1e150 : 1.0);
+            p0 *= s;
+            p1 *= s;
+          }
+        }
       }
     }
     // largest x with cnt <= n-1 becomes lo; smallest x with cnt == n becomes hi
@@ -286,13 +300,14 @@ __device__ __forceinline__ double omega_update(const double* alpha, const double
                                                const double* om_cur, const double* om_prev, double* om_next,
                                                double anorm, int k, int lane) {
   const double eps = 2.220446049250313e-16;
-  const double psi = eps * anorm / beta_j;
+  const double rbj = nr_rcp(beta_j);  // omega is an estimate: the reciprocal's last-bit error is immaterial
+  const double psi = eps * anorm * rbj;
   double mx = 0.0;
   for (int i = lane; i < j; i += 64) {
     double t = beta[i] * om_cur[i + 1] + (alpha[i] - alpha_j) * om_cur[i] -
                (j > 0 ? beta[j - 1] * om_prev[i] : 0.0);
     if (i > 0) t += beta[i - 1] * om_cur[i - 1];
-    t = t / beta_j;
+    t = t * rbj;
     t += t >= 0.0 ? psi : -psi;
     om_next[i] = t;
     mx = fmax(mx, fabs(t));
@@ -402,6 +417,11 @@ __device__ __forceinline__ double nr_transpose_reduce16(const double (&up)[16], 
 // measurement run; no stamp executes otherwise). Thread 0 accumulates shader
 // cycles per phase between the barriers that already delimit the phases.
 __device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memtime(); }
+// Compiled in only by a diagnostic build (make EXTRA=-DNR_STAMPS=1 OUT=...):
+// the stamps' live timer and branches change the profile kernel's register
+// allocation (its spills grew 212 -> 352 B/lane with four more stamp sites,
+// and the kernel ran 30% slower), so the shipped library carries none.
+#ifdef NR_STAMPS
 #define NR_STAMP(slot)                                                          \
   do {                                                                          \
     if (P.stamps && threadIdx.x == 0) {                                         \
@@ -410,6 +430,11 @@ __device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memti
       t_mark = t_;                                                              \
     }                                                                           \
   } while (0)
+#else
+#define NR_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
 
 // Sum of a[r] over lane bits 0..3 (the 16 columns of a tile); lanes with
 // (lane & 3) == 0 end with the total of row group r = 2*b3 + b2, i.e. tile

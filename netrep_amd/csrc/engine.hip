@@ -307,6 +307,27 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   // the dual (S x S) Gram of modules with k > S: the Gram side is min(k, S),
   // and so is every Lanczos dimension (basis columns of that length)
   plan->k_gram = std::min(k_max, n_samples);
+#ifndef NR_SMALL_CLASS
+#define NR_SMALL_CLASS 0
+#endif
+  if (NR_SMALL_CLASS && plan->k_gram <= nr::kSmallDim) {
+    // the small class (kernels.h): several small-workgroup items per CU;
+    // modules longer than its LDS vectors keep their per-node arrays in the
+    // slot's scratch
+    plan->variant = 5;
+    plan->m = nr::kSmallDim;
+    plan->kvec = nr::kSmallDim;
+    plan->big = k_max > nr::kSmallDim;
+    plan->per_cu = nr::profile_small_per_cu();
+    plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * plan->per_cu));
+    plan->gram_doubles = nr::packed_gram_doubles(plan->k_gram + 1);
+    plan->basis_doubles = (int64_t)plan->k_gram * nr::kSmallDim;
+    plan->stride = plan->gram_doubles + plan->basis_doubles + (plan->big ? 5 * (int64_t)k_max : 0);
+    plan->stride = (plan->stride + 31) / 32 * 32;
+    plan->g32_off = plan->stride;
+    plan->stride += (plan->gram_doubles / 2 + 31) / 32 * 32;
+    return NR_OK;
+  }
   const int mg = profile_m_max(plan->k_gram);
   plan->m = mg;
   int kvec = k_max;
@@ -1633,9 +1654,9 @@ int nr_set_stamps(nr_ctx* ctx, int enable) {
   if (!ctx) return NR_ERR_INVALID;
   NR_HIP(ctx, hipSetDevice(ctx->device));
   if (enable && !ctx->d_stamps) {
-    NR_HIP(ctx, hipMalloc((void**)&ctx->d_stamps, 8 * sizeof(unsigned long long)));
+    NR_HIP(ctx, hipMalloc((void**)&ctx->d_stamps, nr::NR_N_STAMPS * sizeof(unsigned long long)));
   }
-  if (enable) NR_HIP(ctx, hipMemset(ctx->d_stamps, 0, 8 * sizeof(unsigned long long)));
+  if (enable) NR_HIP(ctx, hipMemset(ctx->d_stamps, 0, nr::NR_N_STAMPS * sizeof(unsigned long long)));
   if (!enable) dfree(ctx->d_stamps);
   return NR_OK;
 }
@@ -1644,7 +1665,7 @@ int nr_get_stamps(nr_ctx* ctx, uint64_t* cycles) {
   if (!ctx || !cycles) return NR_ERR_INVALID;
   if (!ctx->d_stamps) return fail(ctx, NR_ERR_INVALID, "stamps not enabled");
   NR_HIP(ctx, hipSetDevice(ctx->device));
-  NR_HIP(ctx, hipMemcpy(cycles, ctx->d_stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  NR_HIP(ctx, hipMemcpy(cycles, ctx->d_stamps, nr::NR_N_STAMPS * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return NR_OK;
 }
 

@@ -10,6 +10,19 @@ enum { NR_IDX_PRP = 0, NR_IDX_TABLE = 1, NR_IDX_DIRECT = 2 };
 constexpr int kProfileWaves = 4;  // waves of the 256-thread profile workgroup (NR_WAVES)
 constexpr int kPackedLayoutK = 320;  // modules of the packed kernel's compile-time LDS layout
 
+// phase-stamp slots of the summary-profile kernel (nr_set_stamps)
+constexpr int NR_N_STAMPS = 16;
+
+// The small class of summary-profile items: Lanczos dimension min(k, S) at
+// most kSmallDim, solved by workgroups of kSmallWaves waves (several items per
+// CU in flight instead of three 4-wave items); per-node arrays of modules
+// longer than kSmallDim in the slot's scratch.
+constexpr int kSmallDim = 112;
+#ifndef NR_SMALL_WAVES
+#define NR_SMALL_WAVES 1
+#endif
+constexpr int kSmallWaves = NR_SMALL_WAVES;
+
 // Where the test column of module node c comes from.
 struct IndexSource {
   int mode;                    // NR_IDX_*
@@ -114,7 +127,11 @@ hipError_t launch_gram_full(const double* X, int64_t S, int64_t n, double* gram,
 // out[2e] = in[e], out[2e + 1] = {gram[e], net(j, i)} for e = i + j n.
 hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* out, int64_t n, int symmetric,
                               hipStream_t st);
-// variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch
+// the small class (variant 5): its LDS bytes per workgroup and workgroups per CU
+size_t profile_small_lds();
+int profile_small_per_cu();
+// variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch,
+// 5 the small class
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);
 hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,

@@ -21,6 +21,11 @@
 #include "kernels.h"
 #include "device_common.h"
 
+// Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta.
+#ifndef NR_LZ_TOL
+#define NR_LZ_TOL 5e-15
+#endif
+
 namespace nr {
 
 
@@ -1300,6 +1305,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       if (lane == 0) s_reorth = force_next || mx > sqrt_eps;
     }
     __syncthreads();
+    NR_STAMP(4);  // Lanczos: three-term step + omega recurrence
     if (s_reorth) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
       nb = BF ? reorthogonalise_bf<NW>(Q, k, j + 1, w, h, twork, 5 * mmax, red)  // twork idle until the next check
               : reorthogonalise_cgs<NW>(Q, k, j + 1, w, h, red);
@@ -1315,7 +1321,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       force_next = !force_next;
       if (P.diag && tid == 0) atomicAdd(P.diag + 3, 1);
     }
-    NR_STAMP(4);  // Lanczos: reorthogonalisation
+    NR_STAMP(9);  // Lanczos: reorthogonalisation
     const double beta_j = sqrt(nb);
     if (tid == 0) {
       alpha[j] = alpha_j;
@@ -1343,13 +1349,15 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
         hint_theta = theta;
         hint_r = resid;
         if (lane == 0) {
-          const double tol = 5e-15 * fabs(theta);
+          const double tol = NR_LZ_TOL * fabs(theta);
           const bool conv = resid <= tol;
           s_done = conv || last || !(beta_j > 1e-300 * fabs(theta));
           if (relax && resid <= 1e-7 * fabs(theta)) flags[5] = 1;
           // the Ritz vector's coefficients: inverse iteration (LU), once
           if (s_done) {
+            NR_STAMP(7);
             tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
+            NR_STAMP(12);  // Ritz coefficients (inverse iteration)
             L.h[0] = theta;  // for gv_out (h is idle once the run ends)
           }
           if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
@@ -1371,7 +1379,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       NR_STAMP(7);  // Lanczos: Ritz checks
     }
   }
-  NR_STAMP(2);
+  NR_STAMP(7);
   if (tid == 0 && P.diag) {
     atomicAdd(P.diag + 1, 1);
     atomicAdd(P.diag + 2, nsteps);
@@ -1404,6 +1412,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     }
   }
   __syncthreads();
+  NR_STAMP(10);  // Ritz vector
 }
 
 
@@ -1417,14 +1426,14 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
 // KB > 0 fixes the LDS layout at compile time for modules of at most KB nodes
 // (every carve-out an immediate offset; frees the SGPRs runtime offsets cost).
 // ---------------------------------------------------------------------------
-template <int NW, bool PACKED, int KB>
+template <int NW, bool PACKED, int KB, int MB = 0>
 __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   constexpr int BS = NW * 64;
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_flags[8];
   const int kmax = KB > 0 ? KB : (P.kvec > 0 ? P.kvec : P.k_max);  // LDS vector length
-  const int mmax = KB > 0 ? (KB < 160 ? KB : 160) : P.m_max;
+  const int mmax = KB > 0 ? (MB > 0 ? MB : (KB < 160 ? KB : 160)) : P.m_max;
   const int S = (int)P.n_samples;
   double* part;
   // Large modules (variant 4, !PACKED only): the per-wave matvec partials live
@@ -1517,6 +1526,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
                      : packed_matvec<NW>(G, kc, n, x, out, part, kmax, y, L.red);
       };
       const bool q_given = PACKED && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
+      NR_STAMP(8);  // start column
       const bool gv_rel = !dual;
       lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel);
       relax = false;  // node contributions: the fp64 Gram
@@ -1527,6 +1537,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
           return PACKED ? G[pk_col(c, kc)] : G[c + (int64_t)c * ld];
         }, gv_rel);
       }
+      NR_STAMP(11);  // node contributions
     } else {
       profile_nonfinite<NW>(P, k, m, S, Li);
     }
@@ -1545,6 +1556,16 @@ template <int KB, int OCC>
 __global__ void __launch_bounds__(NR_BS, OCC)
 module_profile_packed4_kernel(ProfileParams P) {
   profile_body<NR_WAVES, true, KB>(P);
+}
+
+// The small class: Lanczos dimension <= kSmallDim (MB = KB = kSmallDim), NW
+// waves per item; three waves per SIMD (HIP's second launch bound is waves per
+// execution unit: the 168-VGPR budget of the packed kernel), as many items
+// per CU as the LDS holds.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64, 3)
+module_profile_small_kernel(ProfileParams P) {
+  profile_body<NW, true, kSmallDim, kSmallDim>(P);
 }
 
 // ---------------------------------------------------------------------------
@@ -1798,6 +1819,19 @@ size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
          sizeof(uint32_t) * k_max;
 }
 
+size_t profile_small_lds() {
+  constexpr int nw = kSmallWaves, kb = kSmallDim, mb = kSmallDim;
+  return sizeof(double) * (8 * nw + 6 * (size_t)kb + packed_part_doubles(nw, kb, mb) + 7 * (size_t)mb + 3) +
+         sizeof(uint32_t) * kb;
+}
+
+// items per CU: the LDS bound, at most 12 waves (the kernel's 168-VGPR budget)
+int profile_small_per_cu() {
+  const int by_lds = (int)((160 * 1024) / profile_small_lds());
+  const int by_waves = 12 / kSmallWaves;
+  return by_lds < by_waves ? by_lds : by_waves;
+}
+
 hipError_t launch_net(const NetParams& P0, int64_t n_items, hipStream_t st) {
   NetParams P = P0;
   P.n_items = n_items;
@@ -1830,6 +1864,11 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
       hipLaunchKernelGGL((module_profile_packed4_kernel<kPackedLayoutK, 3>), g, b4, lds, st, P);
     else
       hipLaunchKernelGGL((module_profile_packed4_kernel<0, 2>), g, b4, lds, st, P);
+    return hipGetLastError();
+  }
+  if (variant == 5) {
+    hipLaunchKernelGGL((module_profile_small_kernel<kSmallWaves>), g, dim3(64 * kSmallWaves),
+                       profile_small_lds(), st, P);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(module_profile_kernel, g, b4, lds, st, P);

@@ -267,9 +267,10 @@ class Engine:
         self._check(self._lib.nr_set_stamps(self._h, int(bool(enable))))
 
     def stamps(self):
-        out = (C.c_uint64 * 8)()
+        out = (C.c_uint64 * 16)()
         self._check(self._lib.nr_get_stamps(self._h, out))
-        names = ["index", "gram", "lanczos_vec", "lanczos_matvec", "reorth", "tail", "beta_sync", "checks"]
+        names = ["index", "gram", "lanczos_init", "lanczos_matvec", "three_term", "stats", "beta_sync", "checks",
+                 "start", "reorth", "ritz_vector", "contrib", "ritz_coeffs", "s13", "s14", "s15"]
         return dict(zip(names, list(out)))
 
     def reset_timing(self):
