@@ -92,6 +92,9 @@ int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric);
  * call whose modules are mostly packed-class items with k <= S; DESIGN.md
  * "Gram table"), else 0. */
 int nr_gram_table(nr_ctx* ctx, int* on);
+/* Wall time in ms of the resident Gram table's build (X^T X on the matrix
+ * cores + the widened layout, synchronised), 0 without a table. */
+int nr_gram_table_ms(nr_ctx* ctx, double* ms);
 
 /* CheckFinite (src/checkFinite.cpp:21-28) of the resident corr and net,
  * computed by nr_set_dataset's symmetry pass over the uploaded matrices (no

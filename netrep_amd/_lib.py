@@ -71,6 +71,7 @@ SIGNATURES = {
     "nr_observed": (_int, [_p, _dp]),
     "nr_observed_async": (_int, [_p]),
     "nr_gram_table": (_int, [_p, C.POINTER(C.c_int)]),
+    "nr_gram_table_ms": (_int, [_p, C.POINTER(C.c_double)]),
     "nr_observed_wait": (_int, [_p, _dp]),
     "nr_run": (_int, [_p, _i64, _i64, _u64, _u32p, _dp]),
     "nr_run_device": (_int, [_p, _i64, _i64, _u64, _p, _p]),

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -47,6 +48,7 @@ struct nr_ctx {
   int32_t pairs_es = 1;          // d_pairs element stride in double2: 2 = the Gram table layout
   double* d_colsum = nullptr;    // [n_nodes] column sums of the data (Gram table)
   int64_t table_checked = -1;    // modules_serial the Gram-table decision was made for
+  double table_ms = 0.0;         // wall time of the last Gram-table build
   double* d_data = nullptr;
   int64_t n_nodes = 0, n_samples = 0;
   std::vector<std::string> node_names;  // column names of a dataset loaded from files
@@ -308,7 +310,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   // and so is every Lanczos dimension (basis columns of that length)
   plan->k_gram = std::min(k_max, n_samples);
 #ifndef NR_SMALL_CLASS
-#define NR_SMALL_CLASS 0
+#define NR_SMALL_CLASS 1
 #endif
   if (NR_SMALL_CLASS && plan->k_gram <= nr::kSmallDim) {
     // the small class (kernels.h): several small-workgroup items per CU;
@@ -654,6 +656,7 @@ int maybe_build_table(nr_ctx* ctx) {
   if (free_b < nn * 40 + ((size_t)1 << 30)) return NR_OK;
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->obs_stream) NR_HIP(ctx, hipStreamSynchronize(ctx->obs_stream));
+  const auto t_build = std::chrono::steady_clock::now();
   double* gram = nullptr;
   double2* tab = nullptr;
   double* cs = nullptr;
@@ -681,6 +684,7 @@ int maybe_build_table(nr_ctx* ctx) {
   ctx->d_pairs = tab;
   ctx->d_colsum = cs;
   ctx->pairs_es = 2;
+  ctx->table_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build).count();
   return NR_OK;
 }
 
@@ -1278,6 +1282,12 @@ int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric) {
 int nr_gram_table(nr_ctx* ctx, int* on) {
   if (!ctx || !on) return NR_ERR_INVALID;
   *on = ctx->d_pairs && ctx->pairs_es == 2 ? 1 : 0;
+  return NR_OK;
+}
+
+int nr_gram_table_ms(nr_ctx* ctx, double* ms) {
+  if (!ctx || !ms) return NR_ERR_INVALID;
+  *ms = ctx->d_pairs && ctx->pairs_es == 2 ? ctx->table_ms : 0.0;
   return NR_OK;
 }
 

@@ -19,7 +19,7 @@ constexpr int NR_N_STAMPS = 16;
 // longer than kSmallDim in the slot's scratch.
 constexpr int kSmallDim = 112;
 #ifndef NR_SMALL_WAVES
-#define NR_SMALL_WAVES 1
+#define NR_SMALL_WAVES 2
 #endif
 constexpr int kSmallWaves = NR_SMALL_WAVES;
 

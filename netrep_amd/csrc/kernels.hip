@@ -1426,7 +1426,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
 // KB > 0 fixes the LDS layout at compile time for modules of at most KB nodes
 // (every carve-out an immediate offset; frees the SGPRs runtime offsets cost).
 // ---------------------------------------------------------------------------
-template <int NW, bool PACKED, int KB, int MB = 0>
+// TABLE: a launch whose items all take the Gram-table path (P.fused, no dual
+// items): the matrix-core and dual Gram code is not compiled in, which lowers
+// the register demand of the kernel (its spills at the 168-VGPR budget).
+template <int NW, bool PACKED, int KB, int MB = 0, bool TABLE = false>
 __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   constexpr int BS = NW * 64;
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
@@ -1476,13 +1479,13 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       Li.q = gnode + 2 * (int64_t)P.k_max;
       Li.w = gnode + 3 * (int64_t)P.k_max;
     }
-    const bool dual = k > S;
+    const bool dual = !TABLE && k > S;
     const int n = dual ? S : k;  // Lanczos dimension
     const int kc = n + 1;
     double g1[1] = {0.0};
     int bad = 0;
     bool gram_done = false;
-    if (PACKED && P.fused && !dual) {
+    if (TABLE || (PACKED && P.fused && !dual)) {
       // Gram table: the item's network statistics from one 32-byte gather per
       // pair, which also carries G_ij -- the packed Gram is filled here (into
       // a zeroed region: padding and the diagonal blocks' upper parts stay 0)
@@ -1508,10 +1511,12 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       for (int64_t i = tid; i < n_part; i += BS) part[i] = 0.0;  // the per-node arrays overlapped them
     }
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
-    if (dual)
-      gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
-    else if (!gram_done)
-      gram_mfma<NW, PACKED>(X, S, L.idx, k, P.ones_off, G, G32, ld, g1[0], bad);
+    if (!TABLE) {
+      if (dual)
+        gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
+      else if (!gram_done)
+        gram_mfma<NW, PACKED>(X, S, L.idx, k, P.ones_off, G, G32, ld, g1[0], bad);
+    }
     if (bad) atomicOr(&s_flags[1], 1);
     block_sums<1, NW>(g1, L.red);  // barriers also publish G to the whole workgroup
     NR_STAMP(1);  // Gram
@@ -1530,7 +1535,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       const bool gv_rel = !dual;
       lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel);
       relax = false;  // node contributions: the fp64 Gram
-      if (dual) {
+      if (!TABLE && dual) {
         profile_contrib_dual<NW>(P, k, m, Li, X, S, g1[0]);
       } else {
         profile_contrib<NW>(P, k, m, L, X, S, g1[0], mv, [&](int c) {
@@ -1556,6 +1561,15 @@ template <int KB, int OCC>
 __global__ void __launch_bounds__(NR_BS, OCC)
 module_profile_packed4_kernel(ProfileParams P) {
   profile_body<NR_WAVES, true, KB>(P);
+}
+
+// The Gram-table launches of the packed class (every item fused, k <= S).
+#ifndef NR_TABLE_KERNEL
+#define NR_TABLE_KERNEL 1
+#endif
+__global__ void __launch_bounds__(NR_BS, 3)
+module_profile_table_kernel(ProfileParams P) {
+  profile_body<NR_WAVES, true, kPackedLayoutK, 0, true>(P);
 }
 
 // The small class: Lanczos dimension <= kSmallDim (MB = KB = kSmallDim), NW
@@ -1860,7 +1874,9 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
     // the compile-time layout of modules of <= 320 nodes at three workgroups
     // per CU (measured fastest: profiles/r02/profile_variants.txt), else the
     // runtime layout
-    if (packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
+    if (NR_TABLE_KERNEL && P.fused && packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
+      hipLaunchKernelGGL(module_profile_table_kernel, g, b4, lds, st, P);
+    else if (packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
       hipLaunchKernelGGL((module_profile_packed4_kernel<kPackedLayoutK, 3>), g, b4, lds, st, P);
     else
       hipLaunchKernelGGL((module_profile_packed4_kernel<0, 2>), g, b4, lds, st, P);

@@ -175,6 +175,12 @@ class Engine:
         self._check(self._lib.nr_gram_table(self._h, C.byref(on)))
         return bool(on.value)
 
+    def gram_table_ms(self) -> float:
+        """Build time of the resident Gram table in ms (nr_gram_table_ms), 0 without one."""
+        ms = C.c_double()
+        self._check(self._lib.nr_gram_table_ms(self._h, C.byref(ms)))
+        return float(ms.value)
+
     def observed_async(self):
         """Enqueue the observed statistics on the context's second stream
         (nr_observed_async); collect them with observed_wait()."""

@@ -1,0 +1,67 @@
+"""The small class of summary-profile items (kernels.h kSmallDim): Lanczos
+dimension min(k, S) <= 112, two-wave workgroups, per-node arrays of modules
+longer than 112 nodes in the slot's scratch. Checked against the C++ LAPACK
+restatement on identical shuffles at the class's edges (k = 112 / 113, k = S,
+dual and primal items in one launch), through the non-finite path, and the
+packed 4-wave kernel's dual path, which the small class now takes over for
+S <= 112, at an S just above it."""
+import numpy as np
+import pytest
+
+import netrep_amd as N
+from oracle import netrep_oracle as O
+
+from conftest import assert_stats_close
+from test_gpu_dual import _case, _cpp
+from test_gpu_parity import _engine_from
+
+pytestmark = pytest.mark.gpu
+
+
+def test_small_class_edges_vs_cpp_oracle():
+    """S = 60: dual items with per-node arrays in scratch (200, 113 > 112),
+    in LDS (112, 61), k == S and primal items (59, 7)."""
+    lay, mi, disc, txs, tc, tn = _case([200, 113, 112, 61, 60, 59, 7], 60, 71, n_nodes=1500)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(5, 29, 123)
+    pis = N.prp_table(123, 5, 29, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (small class)")
+    assert_stats_close(nulls, exp, what="nulls (small class)")
+
+
+def test_small_class_primal_only_vs_cpp_oracle():
+    """S = 300 with every module of at most 112 nodes: primal items of the
+    small class only (Lanczos dimension k)."""
+    lay, mi, disc, txs, tc, tn = _case([112, 96, 64, 33, 16], 300, 73, n_nodes=1200)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(0, 16, 5)
+    pis = N.prp_table(5, 0, 16, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (small class, primal)")
+    assert_stats_close(nulls, exp, what="nulls (small class, primal)")
+
+
+def test_small_class_nonfinite_column_gives_na():
+    """A NaN data column of a module's node: that module's summary-profile
+    statistics are NA (src/netStats.cpp:229-235) on the small class too."""
+    lay, mi, disc, txs, tc, tn = _case([150, 40, 20], 50, 75, n_nodes=600)
+    txs = txs.copy()
+    m0 = mi.mods_present[0]
+    txs[:, mi.test_idx[m0][3]] = np.nan
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    obs = eng.observed()
+    _, exp = O.permutation_procedure(disc, txs, tc, tn, mi, np.zeros((0, mi.null_idx.size), int))
+    assert_stats_close(obs, exp, what="observed with NaN column (small class)")
+    assert not np.isfinite(obs[0, [1, 4, 6]]).any()
+
+
+def test_packed_dual_above_small_class_vs_cpp_oracle():
+    """S = 150 (> 112): dual items (k > S) stay on the packed 4-wave kernel."""
+    lay, mi, disc, txs, tc, tn = _case([300, 220, 151, 150, 90], 150, 77, n_nodes=2000)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(2, 14, 9)
+    pis = N.prp_table(9, 2, 14, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (packed dual)")
+    assert_stats_close(nulls, exp, what="nulls (packed dual)")

@@ -62,7 +62,7 @@ def test_table_with_module_beyond_packed_layout():
 def test_table_asymmetric_network_vs_oracle():
     """net(i, j) != net(j, i): the weighted degrees read net^T from the
     table's fourth slot."""
-    lay, mi, disc, txs, tc, tn = _case([90, 60, 33], 100, 41, n_nodes=500)
+    lay, mi, disc, txs, tc, tn = _case([150, 60, 33], 160, 41, n_nodes=500)
     rng = np.random.default_rng(5)
     tna = tn * (1.0 + 0.05 * rng.random(tn.shape))      # no longer symmetric
     eng = _engine_from(mi, disc, txs, tc, tna)
@@ -81,7 +81,7 @@ def test_table_nonfinite_column_gives_na():
     """A NaN data column shows on the table's diagonal: the module's
     summary-profile statistics are NA (src/netStats.cpp:229-235), its network
     statistics are not affected."""
-    lay, mi, disc, txs, tc, tn = _case([80, 50, 31], 100, 43, n_nodes=500)
+    lay, mi, disc, txs, tc, tn = _case([130, 50, 31], 140, 43, n_nodes=500)
     txs = txs.copy()
     m0 = mi.mods_present[0]
     txs[:, mi.test_idx[m0][2]] = np.nan
