@@ -101,6 +101,8 @@ def parse():
     ap.add_argument("--cpu-baseline-perms", type=int, default=0,
                     help="CPU sample size (0: sized for ~15 s on the host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lib", default=None,
+                    help="tuning A/B only: another build of libnetrep_amd.so (make OUT=... EXTRA=-D...)")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--c5-single", action="store_true",
                     help="C5 as one device-resident test dataset on the engine layer (round 2's C5 record) "
@@ -506,6 +508,8 @@ def run_c5(args, world, rank, local):
 
 def main():
     args = parse()
+    if args.lib:
+        N._lib.LIB_PATH = os.path.abspath(args.lib)
     relaunch_if_needed(args)
     world, rank, local = setup_dist(args)
     if args.config == "C5" and not args.c5_single:
