@@ -60,7 +60,7 @@ def measured_traffic(config, batch, kernel, table=False):
         return None
     for r in rows:
         if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
-                and bool(r.get("gram_table", False)) == table):
+                and bool(r.get("gram_table", False)) == table and "superseded" not in r):
             return float(r["hbm_bytes_per_launch"])
     return None
 
@@ -78,7 +78,8 @@ def measured_mfma(config, batch, kernel, avg_ms, table=False):
         return None
     for r in rows:
         if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
-                and bool(r.get("gram_table", False)) == table and "mfma_f64_flops_executed" in r and avg_ms > 0):
+                and bool(r.get("gram_table", False)) == table and "superseded" not in r
+                and "mfma_f64_flops_executed" in r and avg_ms > 0):
             return {"executed_TFLOPs": round(r["mfma_f64_flops_executed"] / (avg_ms * 1e-3) / 1e12, 4),
                     "mfma_busy_pct": round(r.get("mfma_busy_pct", float("nan")), 2)}
     return None
