@@ -21,6 +21,23 @@
 #include "kernels.h"
 #include "device_common.h"
 
+// the Gram-table items' gathers: pairs per chunk, and whether the next
+// chunk's gathers are issued before the current chunk is processed. Measured
+// (C3 shape, profiles/r03/table_gathers/): 7 pairs 15.86 ms per 256
+// permutations, 5: 15.07, 4: 14.73, 3: 14.41-14.56, 2: 14.27, 1: 14.87; the
+// next chunk in flight adds at most 0.4% (2 pairs: 14.21) for more spill.
+#ifndef NR_TABLE_U
+#define NR_TABLE_U 2
+#endif
+#ifndef NR_TABLE_PIPE
+#define NR_TABLE_PIPE false
+#endif
+
+// the network kernel's gathers: pairs per chunk
+#ifndef NR_NET_U
+#define NR_NET_U 7
+#endif
+
 // Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta.
 #ifndef NR_LZ_TOL
 #define NR_LZ_TOL 5e-15
@@ -419,7 +436,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
       net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch, c);
       net_process<U, true, false>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
     }
-  } else if (GRAM || !PIPE) {
+  } else if (!PIPE) {
     for (int64_t ch = tid; ch < nchunks; ch += BS) {
       NetChunk<U> c;
       net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch, c);
@@ -434,14 +451,14 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     NetChunk<U> a, b;
     const int64_t last = nchunks - 1;
     int64_t ch = tid;
-    net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch, a);
+    net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch, a);
     for (;;) {
-      net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
-      net_process<U, false, false>(P, L, plain_w, cvo, xs, ys, a, acc, go, g1);
+      net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
+      net_process<U, false, GRAM>(P, L, plain_w, cvo, xs, ys, a, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
-      net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
-      net_process<U, false, false>(P, L, plain_w, cvo, xs, ys, b, acc, go, g1);
+      net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
+      net_process<U, false, GRAM>(P, L, plain_w, cvo, xs, ys, b, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
     }
@@ -526,7 +543,7 @@ module_net_kernel(NetParams P) {
     if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
     for (int64_t c = threadIdx.x; c < k; c += NW * 64) L.idx[c] = node_index(P.src, key, p_local, off + c);
     __syncthreads();
-    net_item<NW, NW == 2 || BIG, SYM>(P, m, p_local, off, k, L);
+    net_item<NW, NW == 2 || BIG, SYM, false, NR_NET_U>(P, m, p_local, off, k, L);
   }
 }
 
@@ -1493,10 +1510,25 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       // Lanczos vectors' LDS, idle until the Lanczos phase.
       const GramOut go{G, G32, kc, Sd};
       {
-        const int64_t ng = pk_base(pk_pad(kc) / 16, pk_pad(kc));
-        for (int64_t i = tid; i < ng; i += BS) {
-          G[i] = 0.0;
-          if (G32) G32[i] = 0.0f;
+        // The fill below writes every lower-triangle entry over kc = k + 1
+        // (pairs, diagonal, ones column); zero only what it never writes: the
+        // diagonal blocks' upper parts and the padding rows/columns >= kc.
+        // (Round 3: zeroing the whole packed region first doubled the item's
+        // Gram stores.)
+        const int Pp = pk_pad(kc), ngr = Pp / 16, npad = Pp - kc;
+        for (int i = tid; i < ngr * 256; i += BS) {
+          const int g = i >> 8, r = 16 * g + ((i >> 4) & 15), c = 16 * g + (i & 15);
+          if (r < c || r >= kc || c >= kc) {
+            const int64_t a = pk_at(r, c, kc);
+            G[a] = 0.0;
+            if (G32) G32[a] = 0.0f;
+          }
+        }
+        for (int i = tid; i < (ngr - 1) * npad * 16; i += BS) {  // rows kc.. below the other groups' blocks
+          const int g = i / (npad * 16), rem = i - g * npad * 16;
+          const int64_t a = pk_at(kc + (rem >> 4), 16 * g + (rem & 15), kc);
+          G[a] = 0.0;
+          if (G32) G32[a] = 0.0f;
         }
         __syncthreads();
       }
@@ -1504,7 +1536,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       const NetLds NL = carve_net_over<NW>(L.q, L.red, L.idx, kmax);
       double gp = 0.0;
       int bp = 0;
-      net_item<NW, false, true, true, 7>(P.net, m, p_local, off, k, NL, go, &gp, &bp);
+      net_item<NW, NR_TABLE_PIPE, true, true, NR_TABLE_U>(P.net, m, p_local, off, k, NL, go, &gp, &bp);
       g1[0] = gp;
       bad = bp;
       gram_done = true;
