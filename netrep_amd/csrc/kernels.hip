@@ -38,6 +38,11 @@
 #define NR_NET_U 7
 #endif
 
+// units in flight per wave in the packed matvec's fp64 passes
+#ifndef NR_MV_UF64
+#define NR_MV_UF64 1
+#endif
+
 // Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta.
 #ifndef NR_LZ_TOL
 #define NR_LZ_TOL 5e-15
@@ -1005,7 +1010,7 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
   // loads (32 per lane) before the first wait; the matvec is latency-bound at
   // three workgroups per CU, not byte-bound (profiles/r02/profile_variants.txt).
   // A unit beyond the wave's range loads nothing (range-checked offsets).
-  constexpr int UF = F32 ? 2 : 1;
+  constexpr int UF = F32 ? 2 : NR_MV_UF64;
   using LT = typename std::conditional<F32, float, double>::type;
   for (int u = u0; u < u1; u += UF) {
     LT gb[UF][16];
