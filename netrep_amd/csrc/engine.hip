@@ -424,10 +424,24 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
   if (n_big < n_mod) seg[ns++] = {n_big, n_mod - n_big, {}};
   // every segment's scratch (slots x stride) is one allocation, carved in turn
   int64_t total = 0;
+  bool fuse[2] = {false, false};
   for (int i = 0; i < ns; ++i) {
     const int rc = plan_profile(ctx, (int64_t)seg[i].count * n_perm, k_sorted[seg[i].first], (int)pp.n_samples,
                                 &seg[i].plan);
     if (rc) return rc;
+    // Gram table: the packed class (compile-time layout, no dual items) takes
+    // its network statistics and Gram from the table's gathers, on the table
+    // kernel's own workgroup shape
+    const int k_max = k_sorted[seg[i].first];
+    fuse[i] = table_np && seg[i].plan.variant == 2 && k_max <= nr::kPackedLayoutK && k_max <= pp.n_samples &&
+              nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
+    if (fuse[i] && nr::kTableWaves != nr::kProfileWaves) {
+      int dev_cu = 256;
+      (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+      seg[i].plan.per_cu = nr::profile_table_per_cu();
+      seg[i].plan.slots = (int)std::max<int64_t>(
+          1, std::min<int64_t>((int64_t)seg[i].count * n_perm, (int64_t)dev_cu * seg[i].plan.per_cu));
+    }
     total = std::max<int64_t>(total, seg[i].plan.stride * seg[i].plan.slots);
   }
   // segments run one after the other on one stream: they share the scratch
@@ -448,10 +462,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.part_global = plan.variant == 4 ? 1 : 0;
     pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples);
     pp.g32_off = plan.g32_off;
-    // Gram table: the packed class (compile-time layout, no dual items) takes
-    // its network statistics and Gram from the table's gathers
-    pp.fused = table_np && plan.variant == 2 && k_max <= nr::kPackedLayoutK && k_max <= pp.n_samples &&
-               nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160));
+    pp.fused = fuse[i];
     if (pp.fused) {
       pp.net = *table_np;
       pp.net.mod_order = pp.mod_order;

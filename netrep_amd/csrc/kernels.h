@@ -118,7 +118,15 @@ int profile_kvec_max(int m_max);  // longest LDS vectors of the large-module lay
 hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
 // Whether the packed kernel's LDS (vectors of kvec, basis mmax) holds the
 // network item's per-node arrays (the fused Gram-table path).
-bool fused_net_fits(int kvec, int mmax);
+bool fused_net_fits(int kvec, int mmax, int nw);
+// waves per workgroup of the Gram-table kernel (tuning option NR_TABLE_WAVES),
+// its LDS bytes and workgroups per CU
+#ifndef NR_TABLE_WAVES
+#define NR_TABLE_WAVES 4
+#endif
+constexpr int kTableWaves = NR_TABLE_WAVES;
+size_t profile_table_lds();
+int profile_table_per_cu();
 // The Gram table of a dataset with data: gram[i + j n] = x_i . x_j over the
 // n_samples rows of X (n_samples x (n + 2), the virtual columns behind), and
 // colsum[j] = sum of column j.

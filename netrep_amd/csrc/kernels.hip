@@ -1604,9 +1604,9 @@ module_profile_packed4_kernel(ProfileParams P) {
 #ifndef NR_TABLE_KERNEL
 #define NR_TABLE_KERNEL 1
 #endif
-__global__ void __launch_bounds__(NR_BS, 3)
+__global__ void __launch_bounds__(kTableWaves * 64, 3)
 module_profile_table_kernel(ProfileParams P) {
-  profile_body<NR_WAVES, true, kPackedLayoutK, 0, true>(P);
+  profile_body<kTableWaves, true, kPackedLayoutK, 0, true>(P);
 }
 
 // The small class: Lanczos dimension <= kSmallDim (MB = KB = kSmallDim), NW
@@ -1870,6 +1870,18 @@ size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
          sizeof(uint32_t) * k_max;
 }
 
+size_t profile_table_lds() {
+  constexpr int nw = kTableWaves, kb = kPackedLayoutK, mb = kPackedLayoutK < 160 ? kPackedLayoutK : 160;
+  return sizeof(double) * (8 * nw + 6 * (size_t)kb + packed_part_doubles(nw, kb, mb) + 7 * (size_t)mb + 3) +
+         sizeof(uint32_t) * kb;
+}
+
+int profile_table_per_cu() {
+  const int by_lds = (int)((160 * 1024) / profile_table_lds());
+  const int by_waves = 12 / kTableWaves;
+  return by_lds < by_waves ? by_lds : by_waves;
+}
+
 size_t profile_small_lds() {
   constexpr int nw = kSmallWaves, kb = kSmallDim, mb = kSmallDim;
   return sizeof(double) * (8 * nw + 6 * (size_t)kb + packed_part_doubles(nw, kb, mb) + 7 * (size_t)mb + 3) +
@@ -1912,7 +1924,7 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
     // per CU (measured fastest: profiles/r02/profile_variants.txt), else the
     // runtime layout
     if (NR_TABLE_KERNEL && P.fused && packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
-      hipLaunchKernelGGL(module_profile_table_kernel, g, b4, lds, st, P);
+      hipLaunchKernelGGL(module_profile_table_kernel, g, dim3(64 * kTableWaves), profile_table_lds(), st, P);
     else if (packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
       hipLaunchKernelGGL((module_profile_packed4_kernel<kPackedLayoutK, 3>), g, b4, lds, st, P);
     else
@@ -1952,11 +1964,11 @@ hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* ou
   return hipGetLastError();
 }
 
-bool fused_net_fits(int kvec, int mmax) {
+bool fused_net_fits(int kvec, int mmax, int nw) {
   // NetLds (carve_net_over, from L.q; its reduction scratch is L.red) against
   // the LzLds span from q up to idx (carve_lds, twork in the partials)
-  const size_t need = net_lds_bytes(NR_WAVES, kvec) - sizeof(double) * 8 * NR_WAVES;
-  const size_t have = sizeof(double) * (6 * (size_t)kvec + (size_t)packed_part_doubles(NR_WAVES, kvec, mmax) +
+  const size_t need = net_lds_bytes(nw, kvec) - sizeof(double) * 8 * nw;
+  const size_t have = sizeof(double) * (6 * (size_t)kvec + (size_t)packed_part_doubles(nw, kvec, mmax) +
                                         4 * (size_t)mmax + 3 * ((size_t)mmax + 1));
   return need <= have;
 }
