@@ -1613,8 +1613,11 @@ module_profile_table_kernel(ProfileParams P) {
 // waves per item; three waves per SIMD (HIP's second launch bound is waves per
 // execution unit: the 168-VGPR budget of the packed kernel), as many items
 // per CU as the LDS holds.
+#ifndef NR_SMALL_OCC
+#define NR_SMALL_OCC 3
+#endif
 template <int NW>
-__global__ void __launch_bounds__(NW * 64, 3)
+__global__ void __launch_bounds__(NW * 64, NR_SMALL_OCC)
 module_profile_small_kernel(ProfileParams P) {
   profile_body<NW, true, kSmallDim, kSmallDim>(P);
 }
@@ -1891,7 +1894,7 @@ size_t profile_small_lds() {
 // items per CU: the LDS bound, at most 12 waves (the kernel's 168-VGPR budget)
 int profile_small_per_cu() {
   const int by_lds = (int)((160 * 1024) / profile_small_lds());
-  const int by_waves = 12 / kSmallWaves;
+  const int by_waves = 4 * NR_SMALL_OCC / kSmallWaves;
   return by_lds < by_waves ? by_lds : by_waves;
 }
 
