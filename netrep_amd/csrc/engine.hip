@@ -333,14 +333,30 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   const int mg = profile_m_max(plan->k_gram);
   plan->m = mg;
   int kvec = k_max;
-  if (nr::profile_kernel_lds(kvec, mg, n_samples, 2) > 160 * 1024) variant = 0;
+  plan->big = false;
+#ifndef NR_PACKED_BIG
+#define NR_PACKED_BIG 1
+#endif
+  if (nr::profile_kernel_lds(kvec, mg, n_samples, 2) > 160 * 1024) {
+    // Large modules on the packed Gram too (half the Lanczos bytes of the
+    // full ld x ld Gram): LDS vectors as long as fit, and the per-node arrays
+    // of modules longer than them in the slot's scratch, as long as every
+    // Lanczos dimension min(k, S) fits the vectors.
+    int kp = (k_max + 15) / 16 * 16;
+    while (kp > 16 && nr::profile_kernel_lds(kp, mg, n_samples, 2) > 160 * 1024) kp -= 16;
+    if (NR_PACKED_BIG && plan->k_gram <= kp) {
+      kvec = kp;
+      plan->big = k_max > kp;
+    } else {
+      variant = 0;
+    }
+  }
   // Large modules: the per-wave matvec partials (4 x k doubles) move from LDS
   // to the slot's scratch, which leaves LDS for the six Lanczos vectors only.
   if (variant == 0 && nr::profile_kernel_lds(kvec, mg, n_samples, 0) > 160 * 1024) variant = 4;
   // Modules beyond even those vectors (any k up to N, as src/netStats.cpp:
   // 217-280): Lanczos runs on the dual Gram (dimension S <= kvec) and their
   // per-node arrays live in the slot's scratch.
-  plan->big = false;
   if (variant == 4 && nr::profile_kernel_lds(kvec, mg, n_samples, 4) > 160 * 1024) {
     kvec = nr::profile_kvec_max(mg);
     if (n_samples > kvec)
