@@ -885,6 +885,172 @@ __device__ void gram_mfma(const double* __restrict__ X, int S, const uint32_t* i
 }
 
 
+// One 16 x 16 accumulator tile of column block gc (16 gc .. 16 gc + 15) and
+// row block gr >= gc into the packed layout (pk_store_tile with block indices).
+__device__ __forceinline__ void pk_store_tile16(double* G, float* G32, int kc, int gc, int gr, const nr_f64x4& v,
+                                                int lane) {
+  const int P = pk_pad(kc);
+  const int rb = 16 * (gr - gc);
+  if (rb >= 0 && 16 * gc + rb < P) {
+    const int j = rb >> 6;
+    const int h = min(64, P - 16 * gc - 64 * j);
+    const int i16 = lane & 15, kk = lane >> 4;
+    const int base = (int)pk_base(gc, P) + 1024 * j + (rb & 63) + i16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = kk + 4 * r;
+      const double x = (rb == 0 && i16 < t) ? 0.0 : v[r];  // zero above the diagonal
+      G[base + t * h] = x;
+      if (G32) G32[base + t * h] = (float)x;
+    }
+  }
+}
+
+// The large modules' Gram (primal [X 1]^T[X 1], or the dual H of k > S) in
+// 64 x 64 super-tiles per wave (4 x 4 MFMA tiles; the diagonal super-tiles
+// skip their upper tiles): four times the MFMAs per operand load of the
+// 32 x 32 scheme of gram_mfma / gram_mfma_dual, whose operand streams made the
+// large items' Gram memory-bound (83% of a C5 item, profiles/r03/packed_big).
+// Same operand layout, K order and epilogue as those two; needs the register
+// budget of one wave per SIMD (the large-module kernel runs one workgroup
+// per CU). Packed storage only.
+template <int NW, bool DUAL>
+__device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t* idx, int k, int64_t ones_off,
+                            double* __restrict__ G, float* __restrict__ G32, double& g1sum, int& bad) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int kc = DUAL ? S + 1 : k + 1;
+  const int T4 = (kc + 63) / 64;
+  const int nsup = T4 * (T4 + 1) / 2;
+  const int full = S / 16 * 16;  // primal: steps whose 16 rows are all in range
+  for (int t = wave; t < nsup; t += NW) {
+    int I4 = 0, rem = t;
+    while (rem >= T4 - I4) { rem -= T4 - I4; ++I4; }
+    const int J4 = I4 + rem;
+    const bool diag = I4 == J4;
+    // operand blocks: o < 4 the column side (16 (4 I4 + o) + i16), o >= 4 the row side
+    const double* col[8];
+    int cs[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      const int c = (o < 4 ? 4 * I4 + o : 4 * J4 + o - 4) * 16 + i16;
+      cs[o] = c;
+      if (!DUAL) {
+        const int64_t off = c < k ? (int64_t)idx[c] * S : (c == k ? ones_off : ones_off + S);
+        col[o] = X + off + 4 * kk;
+      }
+    }
+    nr_f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+    auto mfma64 = [&](const double (&v)[8][4]) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            if (!diag || b >= a) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[a][q], v[4 + b][q], acc[a][b], 0, 0, 0);
+    };
+    double cur[8][4], nxt[8][4];
+    if (!DUAL) {
+      auto ld16 = [&](int s0, double (&v)[8][4]) {
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          double2 p0, p1;
+          __builtin_memcpy(&p0, col[o] + s0, sizeof(double2));
+          __builtin_memcpy(&p1, col[o] + s0 + 2, sizeof(double2));
+          v[o][0] = p0.x;
+          v[o][1] = p0.y;
+          v[o][2] = p1.x;
+          v[o][3] = p1.y;
+        }
+      };
+      // two register sets in turn (no copy of the prefetched step)
+      if (full > 0) ld16(0, cur);
+      int s0 = 0;
+      for (; s0 < full; s0 += 32) {
+        if (s0 + 16 < full) ld16(s0 + 16, nxt);
+        mfma64(cur);
+        if (s0 + 16 >= full) { s0 += 16; break; }
+        if (s0 + 32 < full) ld16(s0 + 32, cur);
+        mfma64(nxt);
+      }
+      if (full < S) {  // the last, partial step
+#pragma unroll
+        for (int o = 0; o < 8; ++o)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cur[o][q] = full + 4 * kk + q < S ? col[o][full + q] : 0.0;
+        mfma64(cur);
+      }
+    } else {
+      // operand columns are samples (S: the row sums' all-ones node value,
+      // beyond: zero), the contraction runs over the k nodes, 16 per step.
+      // Super-tiles inside the first S samples (every one but the last row of
+      // them) load unconditionally from the node's column at immediate
+      // offsets; nodes past k load node k-1's values and select zero.
+      const bool interior = 64 * J4 + 64 <= S;
+      auto load = [&](int c0, double (&v)[8][4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = c0 + q;
+          const bool valid = c < k;
+          const double* colp = X + (int64_t)idx[valid ? c : k - 1] * S;
+          if (interior) {
+            const double* pi = colp + 64 * I4 + i16;
+            const double* pj = colp + 64 * J4 + i16;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+              const double xi = pi[16 * o], xj = pj[16 * o];
+              v[o][q] = valid ? xi : 0.0;
+              v[4 + o][q] = valid ? xj : 0.0;
+            }
+          } else {
+#pragma unroll
+            for (int o = 0; o < 8; ++o) {
+              const double x = cs[o] < S ? colp[cs[o]] : (cs[o] == S ? 1.0 : 0.0);
+              v[o][q] = valid ? x : 0.0;
+            }
+          }
+        }
+      };
+      // two register sets in turn (no copy of the prefetched step)
+      load(4 * kk, cur);
+      for (int c0 = 0; c0 < k; c0 += 32) {
+        if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
+        mfma64(cur);
+        if (c0 + 16 >= k) break;
+        if (c0 + 32 < k) load(c0 + 32 + 4 * kk, cur);
+        mfma64(nxt);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (diag && b < a) continue;
+        pk_store_tile16(G, G32, kc, 4 * I4 + a, 4 * J4 + b, acc[a][b], lane);
+        const double wgt = (diag && a == b) ? 1.0 : 2.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // D[row = (lane>>4) + 4r][col = lane & 15] (f64 MFMA C/D map)
+          const int gi = (4 * I4 + a) * 16 + kk + 4 * r;
+          const int gj = (4 * J4 + b) * 16 + i16;
+          const double val = acc[a][b][r];
+          if (DUAL) {
+            if (gj == S && gi < S) g1sum += val * val;  // |X 1|^2 from the row sums
+            if (gi == gj && gi < S) bad |= (int)!isfinite(val);
+          } else {
+            if (gi < k && gj < k) g1sum += wgt * val;
+            if (gi == gj && gi < k) bad |= (int)!isfinite(val);
+          }
+        }
+      }
+  }
+}
+
 // Dual Gram for modules with more nodes than samples (k > S): H = [X' 1]' [X' 1]
 // over the k module nodes, i.e. X X' (S x S) bordered by the row sums X 1 and
 // k. Its top eigenvector is the summary profile u itself (the left singular
@@ -1451,7 +1617,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
 // TABLE: a launch whose items all take the Gram-table path (P.fused, no dual
 // items): the matrix-core and dual Gram code is not compiled in, which lowers
 // the register demand of the kernel (its spills at the 168-VGPR budget).
-template <int NW, bool PACKED, int KB, int MB = 0, bool TABLE = false>
+template <int NW, bool PACKED, int KB, int MB = 0, bool TABLE = false, bool G64 = false>
 __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   constexpr int BS = NW * 64;
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
@@ -1548,7 +1714,12 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       for (int64_t i = tid; i < n_part; i += BS) part[i] = 0.0;  // the per-node arrays overlapped them
     }
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
-    if (!TABLE) {
+    if (G64) {
+      if (dual)
+        gram_mfma64<NW, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
+      else
+        gram_mfma64<NW, false>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad);
+    } else if (!TABLE) {
       if (dual)
         gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
       else if (!gram_done)
@@ -1598,6 +1769,16 @@ template <int KB, int OCC>
 __global__ void __launch_bounds__(NR_BS, OCC)
 module_profile_packed4_kernel(ProfileParams P) {
   profile_body<NR_WAVES, true, KB>(P);
+}
+
+// Packed modules beyond the compile-time layout (runtime LDS layout, one
+// workgroup per CU): the 64 x 64 super-tile Gram at one wave per SIMD.
+#ifndef NR_BIG_G64
+#define NR_BIG_G64 1
+#endif
+__global__ void __launch_bounds__(NR_BS, 1)
+module_profile_big_kernel(ProfileParams P) {
+  profile_body<NR_WAVES, true, 0, 0, false, true>(P);
 }
 
 // The Gram-table launches of the packed class (every item fused, k <= S).
@@ -1930,6 +2111,8 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
       hipLaunchKernelGGL(module_profile_table_kernel, g, dim3(64 * kTableWaves), profile_table_lds(), st, P);
     else if (packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
       hipLaunchKernelGGL((module_profile_packed4_kernel<kPackedLayoutK, 3>), g, b4, lds, st, P);
+    else if (NR_BIG_G64 && wg_per_cu == 1 && !P.fused)
+      hipLaunchKernelGGL(module_profile_big_kernel, g, b4, lds, st, P);
     else
       hipLaunchKernelGGL((module_profile_packed4_kernel<0, 2>), g, b4, lds, st, P);
     return hipGetLastError();
