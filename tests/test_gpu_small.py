@@ -4,7 +4,8 @@ longer than 112 nodes in the slot's scratch. Checked against the C++ LAPACK
 restatement on identical shuffles at the class's edges (k = 112 / 113, k = S,
 dual and primal items in one launch), through the non-finite path, and the
 packed 4-wave kernel's dual path, which the small class now takes over for
-S <= 112, at an S just above it."""
+S <= 112, at an S just above it; the large-module kernel (64 x 64
+super-tile Gram) on primal and dual modules, with non-finite columns."""
 import numpy as np
 import pytest
 
@@ -65,3 +66,33 @@ def test_packed_dual_above_small_class_vs_cpp_oracle():
     exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
     assert_stats_close(eng.observed(), obs, what="observed (packed dual)")
     assert_stats_close(nulls, exp, what="nulls (packed dual)")
+
+
+def test_large_module_kernel_nonfinite_column_gives_na():
+    """The large-module kernel (64 x 64 super-tile Gram, one workgroup per CU
+    at S = 600): a NaN data column in a dual (950-node) and in a primal
+    (580-node) module gives NA summary-profile statistics for those two only."""
+    lay, mi, disc, txs, tc, tn = _case([950, 580, 60], 600, 79, n_nodes=3000)
+    txs = txs.copy()
+    m0, m1 = mi.mods_present[0], mi.mods_present[1]
+    txs[:, mi.test_idx[m0][5]] = np.nan
+    txs[:, mi.test_idx[m1][7]] = np.nan
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    obs = eng.observed()
+    _, exp = O.permutation_procedure(disc, txs, tc, tn, mi, np.zeros((0, mi.null_idx.size), int))
+    assert_stats_close(obs, exp, what="observed with NaN columns (large modules)")
+    for m in (m0, m1):
+        assert not np.isfinite(obs[mi.mods_present.index(m), [1, 4, 6]]).any()
+    assert np.isfinite(obs[mi.mods_present.index(mi.mods_present[2]), [1, 4, 6]]).all()
+
+
+def test_large_module_kernel_vs_cpp_oracle():
+    """S = 600: primal large modules whose Gram side is not a multiple of 64
+    (330, 577) and a dual one (905) on the large-module kernel."""
+    lay, mi, disc, txs, tc, tn = _case([905, 577, 330, 120], 600, 81, n_nodes=3000)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(0, 6, 31)
+    pis = N.prp_table(31, 0, 6, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (large-module kernel)")
+    assert_stats_close(nulls, exp, what="nulls (large-module kernel)")
