@@ -451,6 +451,10 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     const int k_max = k_sorted[seg[i].first];
     fuse[i] = table_np && seg[i].plan.variant == 2 && k_max <= nr::kPackedLayoutK && k_max <= pp.n_samples &&
               nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
+#ifndef NR_TABLE_G32
+#define NR_TABLE_G32 1
+#endif
+    if (fuse[i] && !NR_TABLE_G32) seg[i].plan.g32_off = 0;  // tuning: no fp32 copy, no relaxed steps
     if (fuse[i] && nr::kTableWaves != nr::kProfileWaves) {
       int dev_cu = 256;
       (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
