@@ -480,7 +480,13 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.scratch = *ln.scratch;
     pp.scratch_stride = plan.stride;
     pp.part_global = plan.variant == 4 ? 1 : 0;
-    pp.order_tail = profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples);
+#ifndef NR_ORDER
+#define NR_ORDER 0  // tuning: 0 the cache-budget rule, 1 always module-major, 2 always permutation-major
+#endif
+    pp.order_tail = NR_ORDER == 1 ? 0
+                    : NR_ORDER == 2 ? (int)std::min<int64_t>(n_perm - 1, (plan.slots + seg[i].count - 1) / seg[i].count)
+                                    : profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm,
+                                                         (int)pp.n_samples);
     pp.g32_off = plan.g32_off;
     pp.fused = fuse[i];
     if (pp.fused) {
