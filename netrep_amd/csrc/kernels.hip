@@ -1544,6 +1544,9 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
           // the Ritz vector's coefficients: inverse iteration (LU), once
           if (s_done) {
             NR_STAMP(7);
+            // the Ritz coefficients by inverse iteration (the residual check's
+            // backward recurrence is 2-4% faster but moved statistics by up to
+            // 1.5e-10: profiles/r03/ritz_coefficients/)
             tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
             NR_STAMP(12);  // Ritz coefficients (inverse iteration)
             L.h[0] = theta;  // for gv_out (h is idle once the run ends)
