@@ -369,7 +369,10 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   const size_t lds = nr::profile_kernel_lds(kvec, mg, n_samples, variant);
   if (lds > 160 * 1024)
     return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
-  const int want = variant == 4 ? 1 : 3;
+#ifndef NR_BIG_ALWAYS
+#define NR_BIG_ALWAYS 0  // tuning: every packed launch beyond the 320-node layout on the large-module kernel
+#endif
+  const int want = variant == 4 || (NR_BIG_ALWAYS && variant == 2 && k_max > nr::kPackedLayoutK) ? 1 : 3;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
   plan->variant = variant;
   plan->per_cu = per_cu;

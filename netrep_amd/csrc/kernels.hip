@@ -43,6 +43,12 @@
 #define NR_MV_UF64 1
 #endif
 
+// the large modules' 64 x 64 Gram: prefetched step in a second register set
+// used in turn (1) or copied (0)
+#ifndef NR_G64_PINGPONG
+#define NR_G64_PINGPONG 0
+#endif
+
 // Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta.
 #ifndef NR_LZ_TOL
 #define NR_LZ_TOL 5e-15
@@ -968,15 +974,24 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
           v[o][3] = p1.y;
         }
       };
-      // two register sets in turn (no copy of the prefetched step)
       if (full > 0) ld16(0, cur);
-      int s0 = 0;
-      for (; s0 < full; s0 += 32) {
-        if (s0 + 16 < full) ld16(s0 + 16, nxt);
-        mfma64(cur);
-        if (s0 + 16 >= full) { s0 += 16; break; }
-        if (s0 + 32 < full) ld16(s0 + 32, cur);
-        mfma64(nxt);
+      if (NR_G64_PINGPONG) {  // two register sets in turn (no copy of the prefetched step)
+        for (int s0 = 0; s0 < full; s0 += 32) {
+          if (s0 + 16 < full) ld16(s0 + 16, nxt);
+          mfma64(cur);
+          if (s0 + 16 >= full) break;
+          if (s0 + 32 < full) ld16(s0 + 32, cur);
+          mfma64(nxt);
+        }
+      } else {
+        for (int s0 = 0; s0 < full; s0 += 16) {
+          if (s0 + 16 < full) ld16(s0 + 16, nxt);
+          mfma64(cur);
+#pragma unroll
+          for (int o = 0; o < 8; ++o)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+        }
       }
       if (full < S) {  // the last, partial step
 #pragma unroll
@@ -1016,14 +1031,24 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
           }
         }
       };
-      // two register sets in turn (no copy of the prefetched step)
       load(4 * kk, cur);
-      for (int c0 = 0; c0 < k; c0 += 32) {
-        if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
-        mfma64(cur);
-        if (c0 + 16 >= k) break;
-        if (c0 + 32 < k) load(c0 + 32 + 4 * kk, cur);
-        mfma64(nxt);
+      if (NR_G64_PINGPONG) {  // two register sets in turn (no copy of the prefetched step)
+        for (int c0 = 0; c0 < k; c0 += 32) {
+          if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
+          mfma64(cur);
+          if (c0 + 16 >= k) break;
+          if (c0 + 32 < k) load(c0 + 32 + 4 * kk, cur);
+          mfma64(nxt);
+        }
+      } else {
+        for (int c0 = 0; c0 < k; c0 += 16) {
+          if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
+          mfma64(cur);
+#pragma unroll
+          for (int o = 0; o < 8; ++o)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
+        }
       }
     }
 #pragma unroll
