@@ -46,13 +46,12 @@ FP64_MFMA_PEAK_TFS = 78.6    # MI355X fp64 matrix peak (spec)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def measured_traffic(config, batch, kernel, table=False):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
-    (tools/collect_pmc.sh + tools/summarize_pmc.py: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE, per MI355X_MICROARCH.md). PMC counters cannot be
-    read from inside the timed run, so the number is the one measured on the
-    same command; null when no pass matches this config/batch/kernel (and
-    Gram-table mode: the table kernel's passes carry "gram_table": true)."""
+def _pmc_row(config, batch, kernel, table=False):
+    """The committed rocprofv3 PMC pass (tools/collect_pmc.sh +
+    tools/summarize_pmc.py, recorded by tools/pmc_to_traffic.py) of this
+    config / launch size / kernel, or None. PMC counters cannot be read from
+    inside the timed run, so the numbers are the ones measured on the same
+    command; Gram-table passes carry "gram_table": true."""
     try:
         with open(TRAFFIC_FILE) as f:
             rows = json.load(f)
@@ -61,8 +60,27 @@ def measured_traffic(config, batch, kernel, table=False):
     for r in rows:
         if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
                 and bool(r.get("gram_table", False)) == table and "superseded" not in r):
-            return float(r["hbm_bytes_per_launch"])
+            return r
     return None
+
+
+def traffic_fields(config, batch, kernel, avg_ms, table=False):
+    """Counter traffic per launch of `kernel` from its PMC pass: `traffic` =
+    FETCH_SIZE x 2 + WRITE_SIZE (the gfx950 correction MI355X_MICROARCH.md
+    prescribes for wide streams), `traffic_range` = [raw FETCH_SIZE +
+    WRITE_SIZE, the corrected figure] (the x2 factor is uncalibrated for narrow
+    random gathers), and the pass's rocprofv3 kernel time against this run's
+    HIP-event time (`traffic_time_ratio`: the pass describes this kernel when
+    it is within 2% of 1)."""
+    r = _pmc_row(config, batch, kernel, table)
+    if r is None:
+        return {"traffic": None, "traffic_source": None}
+    raw = (r["fetch_size_kb_raw"] + r["write_size_kb"]) * 1024.0
+    out = {"traffic": float(r["hbm_bytes_per_launch"]), "traffic_range": [raw, float(r["hbm_bytes_per_launch"])],
+           "traffic_source": r.get("source"), "traffic_pass_avg_ms": r["avg_ns_rocprof"] / 1e6}
+    if avg_ms > 0:
+        out["traffic_time_ratio"] = round(r["avg_ns_rocprof"] / 1e6 / avg_ms, 4)
+    return out
 
 
 def measured_mfma(config, batch, kernel, avg_ms, table=False):
@@ -71,18 +89,11 @@ def measured_mfma(config, batch, kernel, avg_ms, table=False):
     as TFLOP/s over this run's HIP-event launch time, and the MFMA-busy share
     (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1,024 SIMDs); None
     when no pass matches."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            rows = json.load(f)
-    except (OSError, ValueError):
+    r = _pmc_row(config, batch, kernel, table)
+    if r is None or "mfma_f64_flops_executed" not in r or avg_ms <= 0:
         return None
-    for r in rows:
-        if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
-                and bool(r.get("gram_table", False)) == table and "superseded" not in r
-                and "mfma_f64_flops_executed" in r and avg_ms > 0):
-            return {"executed_TFLOPs": round(r["mfma_f64_flops_executed"] / (avg_ms * 1e-3) / 1e12, 4),
-                    "mfma_busy_pct": round(r.get("mfma_busy_pct", float("nan")), 2)}
-    return None
+    return {"executed_TFLOPs": round(r["mfma_f64_flops_executed"] / (avg_ms * 1e-3) / 1e12, 4),
+            "mfma_busy_pct": round(r.get("mfma_busy_pct", float("nan")), 2), "source": r.get("source")}
 
 
 def parse():
@@ -492,18 +503,41 @@ def run_c5(args, world, rank, local):
         nk["gather_ceiling"] = gather_ceiling(sizes, P / max(l0, 1), ms0 / max(l0, 1) / 1e3)
         nk["gather_ceiling"]["peak_c5_footprint"] = GATHER_CEILING_C5_GREADS
         nk["gather_ceiling"]["frac_c5_footprint"] = nk["gather_ceiling"]["achieved"] / GATHER_CEILING_C5_GREADS
-    # the dominant kernel (the summary-profile launches of one batch)
+    # the dominant kernel (the summary-profile launches of one batch: the
+    # large modules' Gram executes on the matrix cores)
     b_launch = int(round(P / max(l1, 1)))
     if mk["achieved"] is not None:
+        avg1 = ms1 / max(l1, 1)
         line["roofline"] = {"kernel": "module_profile_kernel", "bound": "mfma", "achieved": round(mk["achieved"], 4),
                             "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(mk["frac"], 6),
-                            "traffic": measured_traffic("C5", b_launch, "module_profile_kernel"),
-                            "traffic_unit": "L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 "
-                                            "+ WRITE_SIZE, profiles/pmc_traffic.json)",
-                            "algorithmic_bytes": round(prof_b * b_launch), "launch_permutations": b_launch,
-                            "executed": measured_mfma("C5", b_launch, "module_profile_kernel", ms1 / max(l1, 1))}
-    line["cpu_baseline"] = None
-    line["cpu_baseline_note"] = "the default bench line (C3) carries the CPU baseline"
+                            "avg_ms": avg1, "algorithmic_bytes": round(prof_b * b_launch),
+                            "launch_permutations": b_launch,
+                            "units_note": "achieved = SURVEY.md 8d Gram flops F(k) = 2 S k min(S,k) per "
+                                          "module-permutation x the launch's items / HIP-event launch time"}
+        line["roofline"].update(traffic_fields("C5", b_launch, "module_profile_kernel", avg1))
+        line["roofline"]["traffic_unit"] = ("L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE "
+                                            "x2 + WRITE_SIZE; traffic_range = [raw, x2]; profiles/pmc_traffic.json)")
+        line["roofline"]["executed"] = measured_mfma("C5", b_launch, "module_profile_kernel", avg1)
+    cpu = None
+    if not args.no_cpu_baseline:
+        # the C++ restatement on the same resident-dataset index sets (dataset 0,
+        # null = "all": the pool is every test gene), one permutation per thread
+        from oracle import ref_cpp
+        hc = host_cores()
+        threads = max(1, min(hc["lease_share"], hc["affinity"]))
+        n_cpu = args.cpu_baseline_perms or threads
+        t1 = time.perf_counter()
+        ref_cpp.permutation_procedure(x.f, c.f, nt.f, len(modules), np.arange(len(modules)), node_off, idx_t, idx_t,
+                                      np.arange(n), v["corr"], v["degree"], v["contribution"], n_cpu, seed=seed,
+                                      n_threads=threads, want_observed=False)
+        dt = time.perf_counter() - t1
+        cpu = {"value": n_cpu / dt, "unit": "permutations/sec", "cores": threads, "kind": "port",
+               "per_core": n_cpu / dt / threads,
+               "host": {"cpu_model": hc["model"], "nproc": hc["nproc"], "affinity": hc["affinity"],
+                        "lease_share": hc["lease_share"], "whole_host_estimate": n_cpu / dt / threads * hc["nproc"]},
+               "sample": f"{n_cpu} permutations x {len(modules)} modules of test dataset 0 in {dt:.1f} s: C++ "
+                         f"restatement of src/permutations.cpp (std::thread chunks, LAPACK SVD), {threads} threads"}
+    line["cpu_baseline"] = cpu
     print(json.dumps(line))
 
 
@@ -568,10 +602,10 @@ def main():
                 "roofline": {"kernel": "module_net_kernel", "bound": "hbm", "avg_ms": ms2 / max(l2, 1),
                              "achieved": net_b * B2 / t2 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": net_b * B2 / t2 / 1e9 / HBM_PEAK_GBS,
-                             "traffic": measured_traffic("C4", B2, "module_net_kernel"),
                              "algorithmic_bytes": round(net_b * B2)},
                 "gather_ceiling": gather_ceiling(lay.module_sizes, B2, t2),
             }
+            secondary["roofline"].update(traffic_fields("C4", B2, "module_net_kernel", ms2 / max(l2, 1)))
         eng2.close()
 
     if rank == 0:
@@ -580,30 +614,35 @@ def main():
         kernels = {}
         fused = meta["with_data"] and l0 == 0   # network statistics computed inside the profile kernel
         if l0 > 0:
+            t0 = ms0 / l0 / 1e3
             kernels["module_net_kernel"] = {
                 "bound": "hbm", "avg_ms": ms0 / l0, "launches": l0,
-                "achieved": net_b * B / (ms0 / l0 / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "gather_ceiling": gather_ceiling(lay.module_sizes, B, ms0 / l0 / 1e3)}
+                "achieved": net_b * B / t0 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "algorithmic_bytes": round(net_b * B),
+                "gather_ceiling": gather_ceiling(lay.module_sizes, B, t0)}
         table = meta["with_data"] and eng.gram_table()
         if table:
             # Gram table: every statistic of a module-permutation in this one
             # launch -- network values and the packed Gram from one 32-byte
-            # table gather per pair, then the Lanczos eigenpair. The roofline
-            # keeps SURVEY.md 8d's algorithmic units (Gram flops F(k), bytes
-            # B(k)); the Gram flops are served by the per-dataset table X^T X
-            # (2 S n^2 once) instead of being executed per item.
+            # table gather per pair, then the Lanczos eigenpair. The kernel
+            # executes no MFMA (its Gram comes from the per-dataset table), so
+            # it is a memory kernel: the primary figure is SURVEY.md 8d's
+            # algorithmic bytes B(k) per launch against HBM peak; the Gram
+            # flops F(k) the table serves stay as a secondary figure.
             t1 = ms1 / max(l1, 1) / 1e3
             tab_b = table_bytes(lay.module_sizes)
             kernels["module_profile_kernel"] = {
-                "bound": "mfma", "avg_ms": ms1 / max(l1, 1), "launches": l1,
-                "achieved": prof_f * B / t1 / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "bound": "hbm", "avg_ms": ms1 / max(l1, 1), "launches": l1,
+                "achieved": (net_b + prof_b) * B / t1 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "algorithmic_bytes": round((net_b + prof_b) * B),
+                "units_note": "achieved = SURVEY.md 8d algorithmic bytes B(k) = 4k + 8k(k-1)/2 + 8k^2 + 8Sk per "
+                              "module-permutation x the launch's items / HIP-event launch time",
                 "gram_table": True, "fused_network_statistics": fused,
-                "units_note": "achieved = SURVEY.md 8d algorithmic Gram flops F(k) = 2 S k min(S,k) per "
-                              "module-permutation / launch time; per item they come from the dataset's Gram "
-                              "table (2 S n^2 flops once per dataset), not from executed MFMA",
-                "hbm": {"achieved": (net_b + prof_b) * B / t1 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": (net_b + prof_b) * B / t1 / 1e9 / HBM_PEAK_GBS,
-                        "note": "SURVEY.md 8d algorithmic bytes B(k) incl. 8 S k data bytes"},
+                "f_units": {"achieved": prof_f * B / t1 / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                            "frac": prof_f * B / t1 / 1e12 / FP64_MFMA_PEAK_TFS,
+                            "note": "secondary: SURVEY.md 8d Gram flops F(k) = 2 S k min(S,k) per module-permutation "
+                                    "/ launch time; served by the dataset's Gram table (2 S n^2 flops once per "
+                                    "dataset), not executed per item (executed MFMA: roofline.executed)"},
                 "table_gather_bytes": {"achieved": tab_b * B / t1 / 1e9, "unit": "GB/s",
                                        "note": "32-byte table element per pair and diagonal entry + indices + "
                                                "discovery vectors, the bytes this kernel's gathers need"},
@@ -611,14 +650,17 @@ def main():
                 "table_build_ms": eng.gram_table_ms(),
                 "table_build_note": "one-off per test dataset, in the first (warm-up) run: X^T X on the "
                                     "matrix cores + the widened {corr, net, gram, net^T} layout; outside "
-                                    "the timed steps like the dataset upload"}
+                                    "the timed steps like the dataset upload (it is "
+                                    f"{eng.gram_table_ms() / (elapsed * 1e3) * 100:.2f}% of this run's timed region)"}
         elif meta["with_data"]:
             t1 = ms1 / max(l1, 1) / 1e3
             kernels["module_profile_kernel"] = {
                 "bound": "mfma", "avg_ms": ms1 / max(l1, 1), "launches": l1,
                 "achieved": prof_f * B / t1 / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "fused_network_statistics": fused,
-                # algorithmic HBM bytes the launch moves (gathers + data columns) per its duration
+                "units_note": "achieved = SURVEY.md 8d Gram flops F(k) = 2 S k min(S,k) per module-permutation "
+                              "x the launch's items / HIP-event launch time (executed on the matrix cores)",
+                "algorithmic_bytes": round(((net_b if fused else 0.0) + prof_b) * B),
                 "hbm_achieved_GBps": ((net_b if fused else 0.0) + prof_b) * B / t1 / 1e9}
         for kv in kernels.values():
             kv["frac"] = kv["achieved"] / kv["peak"]
@@ -626,19 +668,15 @@ def main():
         dom = kernels[dom_name]
         roofline = {"kernel": dom_name, "bound": dom["bound"], "achieved": round(dom["achieved"], 4),
                     "peak": dom["peak"], "unit": dom["unit"], "frac": round(dom["frac"], 6),
-                    "traffic": measured_traffic(args.config, B, dom_name, bool(table)),
-                    "traffic_unit": "L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 "
-                                    "+ WRITE_SIZE, profiles/pmc_traffic.json)",
-                    "algorithmic_bytes": round(((net_b if fused or dom_name == "module_net_kernel" else 0.0)
-                                                + (prof_b if dom_name == "module_profile_kernel" else 0.0)) * B)}
+                    "avg_ms": dom["avg_ms"], "algorithmic_bytes": dom["algorithmic_bytes"],
+                    "units_note": dom.get("units_note")}
+        roofline.update(traffic_fields(args.config, B, dom_name, dom["avg_ms"], bool(table)))
+        roofline["traffic_unit"] = ("L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 + "
+                                    "WRITE_SIZE; traffic_range = [raw, x2]; profiles/pmc_traffic.json)")
         if table and dom_name == "module_profile_kernel":
-            roofline["gram_table"] = True
-            roofline["units_note"] = dom["units_note"]
-            roofline["hbm"] = dom["hbm"]
-            roofline["gather_ceiling"] = dom["gather_ceiling"]
-            roofline["table_build_ms"] = dom["table_build_ms"]
-        if dom["unit"] == "TFLOP/s":  # executed MFMA flops next to the algorithmic figure (PMC pass)
-            roofline["executed"] = measured_mfma(args.config, B, dom_name, dom.get("avg_ms", 0.0), bool(table))
+            for key in ("gram_table", "f_units", "gather_ceiling", "table_build_ms"):
+                roofline[key] = dom[key]
+        roofline["executed"] = measured_mfma(args.config, B, dom_name, dom["avg_ms"], bool(table))
         cpu = None
         if world == 1 and not args.no_cpu_baseline and host is not None:
             rate, dt, n_cpu, threads, hc = cpu_baseline(lay, meta, host, args.cpu_baseline_perms, args.seed)

@@ -30,10 +30,10 @@ extern "C" {
 #define NR_ERR_HIP 1          /* HIP runtime / launch failure */
 #define NR_ERR_INVALID 2      /* bad argument, shape or missing prerequisite */
 #define NR_ERR_OOM 3          /* device allocation failed */
-#define NR_ERR_UNSUPPORTED 4  /* size beyond an engine limit: a module of more nodes than the
-                                 summary-profile kernel's LDS vectors hold (~2,500) in a dataset
-                                 of more samples than that (modules of any size are accepted
-                                 otherwise, as src/netStats.cpp:217-280) */
+#define NR_ERR_UNSUPPORTED 4  /* size beyond an engine limit (n_nodes >= 2^31); modules of any
+                                 size and any sample count are accepted, as svd_econ accepts any
+                                 S x k block (src/netStats.cpp:217-280): Lanczos dimensions beyond
+                                 the LDS vectors keep their vectors in device scratch */
 #define NR_ERR_CANCELLED 5    /* nr_cancel() was called during a run */
 #define NR_ERR_NONFINITE 6    /* CheckFinite failure (src/checkFinite.cpp:25-27) */
 
@@ -62,10 +62,17 @@ const char* nr_last_error(const nr_ctx* ctx);
  * CorrVector (src/netStats.cpp:196-201) and WeightedDegree (:135). */
 int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net,
                    const double* data, int64_t n_nodes, int64_t n_samples, int where);
+/* The same with flags: NR_SCALE_DATA = `data` is unscaled and is scaled on
+ * the device (Scale, src/scale.cpp:14-25) on its way into HBM (NetProps,
+ * src/properties.cpp:49). corr == net (same pointer): the matrix crosses
+ * PCIe once and fills both halves of the pairs. */
+#define NR_SCALE_DATA 1
+int nr_set_dataset_ex(nr_ctx* ctx, const double* corr, const double* net,
+                      const double* data, int64_t n_nodes, int64_t n_samples, int where, int flags);
+/* Drop the resident dataset (and modules / null pool bound to it); the
+ * context keeps its streams and scratch for the next dataset. */
+int nr_clear_dataset(nr_ctx* ctx);
 
-/* Make src's resident dataset resident in dst too, device to device (over
- * xGMI when the contexts are on different GPUs): the host matrices cross PCIe
- * once, to the first GPU, and fan out from there (SURVEY.md 8e). */
 /* disk.matrix files straight to HBM (R/disk-matrix-class.R:175-182 reads them
  * back with readRDS): numeric matrices serialised by saveRDS (gzip or
  * uncompressed, XDR format 2/3) or objects of a save() archive (`*_object`,
@@ -82,15 +89,28 @@ int nr_dataset_shape(const nr_ctx* ctx, int64_t* n_nodes, int64_t* n_samples);
  * (written only when cap >= *needed). */
 int nr_dataset_colnames(const nr_ctx* ctx, char* buf, int64_t cap, int64_t* needed);
 
+/* Make src's resident dataset resident in dst too, device to device (over
+ * xGMI when the contexts are on different GPUs): the host matrices cross PCIe
+ * once, to the first GPU, and fan out from there (SURVEY.md 8e). */
 int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src);
+/* ctxs[0]'s resident dataset to ctxs[1..n): the broadcast of SURVEY.md 8e as
+ * a scatter + all-gather of peer copies over the full xGMI mesh (each
+ * destination receives one piece from the source and the other n - 2 pieces
+ * from the destinations that received them; every link carries 1/(n-1) of
+ * the bytes per phase). Contexts must be distinct; several may share a GPU. */
+int nr_broadcast_dataset(nr_ctx* const* ctxs, int n);
 
 /* 1 if corr and net of the resident dataset are exactly symmetric. */
 int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric);
 
 /* 1 when the resident dataset carries the Gram table (the data block's
  * X^T X interleaved with the matrices, built by the first run or observed
- * call whose modules are mostly packed-class items with k <= S; DESIGN.md
- * "Gram table"), else 0. */
+ * call), else 0. Whether it is built depends on the shapes only (never on
+ * free device memory): the packed-class modules (<= 320 nodes) must form one
+ * packed-kernel launch (min(k, S) > 112, no module with more nodes than
+ * samples), carry at least half the Gram work, and n_nodes <= 50,000; an
+ * allocation failure then returns NR_ERR_OOM from the run / observed call
+ * (DESIGN.md section 5.2). */
 int nr_gram_table(nr_ctx* ctx, int* on);
 /* Wall time in ms of the resident Gram table's build (X^T X on the matrix
  * cores + the widened layout, synchronised), 0 without a table. */
@@ -202,9 +222,16 @@ int nr_cancel(nr_ctx* ctx);
 
 /* Tuning and measurement. */
 int nr_set_batch(nr_ctx* ctx, int64_t perms_per_launch);
-/* Host threads of the pinned staging copies (process-wide; n <= 0: 8, the
- * default; capped at 16). The reference-interface calls set it from n_cores. */
+/* Host threads of the staging copies: the process-wide default for contexts
+ * created afterwards (n <= 0: 8; capped at 16), and one context's own count.
+ * The reference-interface calls set their contexts' count from n_cores and
+ * never change the process default. */
 int nr_set_host_threads(int n);
+int nr_ctx_set_host_threads(nr_ctx* ctx, int n);
+/* Host -> device bytes the library has copied since it was loaded (every
+ * upload path counts): a caller can verify that resident data is not
+ * uploaded again. */
+int nr_h2d_bytes(int64_t* bytes);
 int nr_set_timing(nr_ctx* ctx, int enable);
 /* Accumulated device time (HIP events on the launch stream) per kernel:
  * kernel 0 = module network statistics, 1 = summary-profile statistics. */
@@ -375,6 +402,19 @@ int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes,
 /* CheckFinite (src/checkFinite.cpp:21-28): NR_ERR_NONFINITE with the
  * reference's message if any element is NA/NaN/Inf. */
 int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol);
+
+/* Residency across calls of the reference-interface layer (modulePreservation
+ * calls IntermediateProperties and PermutationProcedure once per (discovery,
+ * test) pair, R/modulePreservation.R:553-635; networkProperties calls NetProps
+ * once per pair, R/networkProperties.R:295-302): the discovery dataset of
+ * netrep_IntermediateProperties and the dataset of netrep_NetProps stay
+ * resident in HBM while later calls name the same host arrays (same
+ * pointers and shape, and the same sampled fingerprint of their contents);
+ * contexts (streams, slot scratch) are pooled across calls. The arrays must
+ * not change between calls that should reuse them. netrep_ReleaseResident
+ * frees all of it (the R glue calls it when modulePreservation /
+ * networkProperties return). */
+void netrep_ReleaseResident(void);
 
 /* Last error of the reference-interface layer (thread-local). */
 const char* netrep_last_error(void);

@@ -10,7 +10,7 @@ The compute path is the HIP library ``netrep_amd/_lib/libnetrep_amd.so``.
 from ._lib import NetRepError, load  # noqa: F401
 from .api import (CheckFinite, IntermediateProperties, IntermediatePropertiesNoData,  # noqa: F401
                   NetProps, NetPropsNoData, PermutationProcedure, PermutationProcedureNoData,
-                  PrefetchTestDataset, DiscardPrefetch, PermutationProcedureFiles, RMatrix,
+                  PrefetchTestDataset, DiscardPrefetch, ReleaseResident, h2d_bytes, PermutationProcedureFiles, RMatrix,
                   read_rds_matrix, Scale, STATNAMES, STATNAMES_NODATA,
                   set_interrupt_hook)
 from .engine import Engine, device_count, prp_table  # noqa: F401
@@ -19,4 +19,4 @@ __all__ = ["CheckFinite", "IntermediateProperties", "IntermediatePropertiesNoDat
            "NetPropsNoData", "PermutationProcedure", "PermutationProcedureNoData", "RMatrix",
            "Scale", "Engine", "NetRepError", "device_count", "prp_table", "STATNAMES",
            "STATNAMES_NODATA", "set_interrupt_hook", "PrefetchTestDataset",
-           "DiscardPrefetch", "PermutationProcedureFiles", "read_rds_matrix"]
+           "DiscardPrefetch", "ReleaseResident", "h2d_bytes", "PermutationProcedureFiles", "read_rds_matrix"]

@@ -25,6 +25,7 @@ NR_ERR_CANCELLED = 5
 NR_ERR_NONFINITE = 6
 NR_HOST = 0
 NR_DEVICE = 1
+NR_SCALE_DATA = 1
 
 
 class NetRepError(RuntimeError):
@@ -63,6 +64,12 @@ SIGNATURES = {
     "nr_ctx_destroy": (None, [_p]),
     "nr_last_error": (C.c_char_p, [_p]),
     "nr_set_dataset": (_int, [_p, _dp, _dp, _dp, _i64, _i64, _int]),
+    "nr_set_dataset_ex": (_int, [_p, _dp, _dp, _dp, _i64, _i64, _int, _int]),
+    "nr_clear_dataset": (_int, [_p]),
+    "nr_broadcast_dataset": (_int, [C.POINTER(_p), _int]),
+    "nr_ctx_set_host_threads": (_int, [_p, _int]),
+    "nr_h2d_bytes": (_int, [_i64p]),
+    "netrep_ReleaseResident": (None, []),
     "nr_copy_dataset": (_int, [_p, _p]),
     "nr_dataset_symmetric": (_int, [_p, _intp]),
     "nr_dataset_finite": (_int, [_p, _intp, _intp]),

@@ -269,6 +269,23 @@ def DiscardPrefetch() -> None:
     _prefetched.clear()
 
 
+def ReleaseResident() -> None:
+    """Free the datasets kept resident between calls (IntermediateProperties'
+    discovery dataset, NetProps' dataset), pending prefetches and the pooled
+    contexts (netrep_ReleaseResident; the R glue calls it when
+    modulePreservation / networkProperties return)."""
+    L.load().netrep_ReleaseResident()
+    _prefetched.clear()
+
+
+def h2d_bytes() -> int:
+    """Host -> device bytes the library has copied since it was loaded
+    (nr_h2d_bytes): the difference across calls shows what was uploaded."""
+    v = C.c_int64()
+    L.check(L.load().nr_h2d_bytes(C.byref(v)))
+    return int(v.value)
+
+
 def _permutation(disc_props, t_data, t_corr, t_net, module_assignments, modules, n_perm, n_cores,
                  null_hypothesis, verbose, seed, pi):
     lib = L.load()

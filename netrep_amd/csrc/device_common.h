@@ -498,6 +498,32 @@ __device__ __forceinline__ LzLds carve_lds(unsigned char* smem, int kvec, int mm
   return L;
 }
 
+// Variant 6 (Lanczos dimensions beyond the LDS vectors): only the reduction
+// scratch and the tridiagonal arrays in LDS; the six vectors (kvec each) and
+// the index set in the slot's global scratch at `gvec` (the workgroup's
+// barriers order them: one CU, one vector L1). Same roles as carve_lds with
+// twork outside the partials.
+template <int NW>
+__device__ __forceinline__ LzLds carve_split(unsigned char* smem, double* gvec, int kvec, int mmax) {
+  LzLds L;
+  L.red = reinterpret_cast<double*>(smem);  // 8 * NW
+  L.alpha = L.red + 8 * NW;
+  L.beta = L.alpha + mmax;
+  L.h = L.beta + mmax;
+  L.ty = L.h + mmax;
+  L.twork = L.ty + mmax;                    // [5 * mmax]
+  L.omg = L.twork + 5 * mmax;               // [3 * (mmax + 1)]
+  L.q = gvec;
+  L.qprev = L.q + kvec;
+  L.w = L.qprev + kvec;
+  L.vv = L.w + kvec;
+  L.gv = L.vv + kvec;
+  L.colm = L.gv + kvec;
+  L.idx = reinterpret_cast<uint32_t*>(L.colm + kvec);
+  L.mmax = mmax;
+  return L;
+}
+
 // Node contributions from the Ritz vector (u = X v / sigma):
 //   NC_j = cor(x_j, u) = ((Gv)_j/sigma - S m_j ubar) / sqrt((G_jj - S m_j^2)(1 - S ubar^2)),
 // oriented by sign(cor(rowMeans(X), u)) (src/netStats.cpp:242-247, 279); the

@@ -29,6 +29,14 @@ namespace {
 
 thread_local std::string g_create_error;
 
+// Host -> device bytes moved by the library since it was loaded (nr_h2d_bytes):
+// every upload path adds what it copies, so a caller can check that a
+// resident dataset is not uploaded again.
+std::atomic<int64_t> g_h2d_bytes{0};
+
+// Default host threads of the staging copies for new contexts (nr_set_host_threads).
+std::atomic<int> g_host_threads{8};
+
 struct DeviceTimer {
   double ms = 0.0;
   int64_t launches = 0;
@@ -42,6 +50,7 @@ struct nr_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   std::mutex mu;
+  int host_threads = 8;  // host threads of this context's staging copies (nr_ctx_set_host_threads)
 
   // resident dataset
   double2* d_pairs = nullptr;
@@ -148,12 +157,18 @@ void dfree(T*& p) {
   p = nullptr;
 }
 
+// Every host -> device copy of the library goes through here (counted).
+hipError_t h2d_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  g_h2d_bytes.fetch_add((int64_t)bytes);
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+}
+
 template <typename T>
 int upload(nr_ctx* ctx, T*& dst, const T* src, size_t n) {
   dfree(dst);
   if (n == 0 || src == nullptr) return NR_OK;
   NR_HIP(ctx, hipMalloc((void**)&dst, n * sizeof(T)));
-  NR_HIP(ctx, hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  NR_HIP(ctx, h2d_async(dst, src, n * sizeof(T), ctx->stream));
   return NR_OK;
 }
 
@@ -248,7 +263,9 @@ int gram_ld(int k_max) { return (k_max + 1 + 31) / 32 * 32; }
 //   variant 0: the full Gram, where the packed layout's LDS does not fit;
 //   variant 4: the full Gram with the matvec partials in scratch, where even
 //              that does not fit; `big`: the per-node arrays in scratch too
-//              (modules beyond the LDS vectors; dual Gram only).
+//              (modules beyond the LDS vectors; dual Gram only);
+//   variant 6: variant 4 with every Lanczos vector and the index set in
+//              scratch (Lanczos dimension min(k, S) beyond the LDS vectors).
 // Modules with k > S use the S x S dual Gram. One numerical path per layout:
 // no run-time switch selects another (round-2 A/B variants are compile-time
 // history, profiles/r02/profile_variants.txt and profiles/r03/).
@@ -356,14 +373,18 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   if (variant == 0 && nr::profile_kernel_lds(kvec, mg, n_samples, 0) > 160 * 1024) variant = 4;
   // Modules beyond even those vectors (any k up to N, as src/netStats.cpp:
   // 217-280): Lanczos runs on the dual Gram (dimension S <= kvec) and their
-  // per-node arrays live in the slot's scratch.
+  // per-node arrays live in the slot's scratch; where the Lanczos dimension
+  // min(k, S) itself can exceed the LDS vectors (S > kvec), every vector and
+  // the index set move to the slot's scratch too (variant 6: no size limit
+  // but device memory).
   if (variant == 4 && nr::profile_kernel_lds(kvec, mg, n_samples, 4) > 160 * 1024) {
     kvec = nr::profile_kvec_max(mg);
-    if (n_samples > kvec)
-      return fail(ctx, NR_ERR_UNSUPPORTED,
-                  "module of more than " + std::to_string(kvec) + " nodes needs the dual Gram and at most " +
-                      std::to_string(kvec) + " samples");
-    plan->big = true;
+    if (n_samples > kvec) {
+      variant = 6;
+      kvec = k_max;
+    } else {
+      plan->big = true;
+    }
   }
   plan->kvec = kvec;
   const size_t lds = nr::profile_kernel_lds(kvec, mg, n_samples, variant);
@@ -372,7 +393,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
 #ifndef NR_BIG_ALWAYS
 #define NR_BIG_ALWAYS 0  // tuning: every packed launch beyond the 320-node layout on the large-module kernel
 #endif
-  const int want = variant == 4 || (NR_BIG_ALWAYS && variant == 2 && k_max > nr::kPackedLayoutK) ? 1 : 3;
+  const int want = variant == 4 || variant == 6 || (NR_BIG_ALWAYS && variant == 2 && k_max > nr::kPackedLayoutK) ? 1 : 3;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
   plan->variant = variant;
   plan->per_cu = per_cu;
@@ -386,8 +407,9 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   }
   plan->basis_doubles = (int64_t)plan->k_gram * mg;
   plan->stride = plan->gram_doubles + plan->basis_doubles +
-                 (variant == 4 ? (int64_t)nr::kProfileWaves * kvec : 0) +
-                 (plan->big ? 5 * (int64_t)k_max : 0);  // x.u, means, squares, contributions, index set
+                 (variant == 4 || variant == 6 ? (int64_t)nr::kProfileWaves * kvec : 0) +
+                 (plan->big ? 5 * (int64_t)k_max : 0) +  // x.u, means, squares, contributions, index set
+                 (variant == 6 ? 6 * (int64_t)kvec + (kvec + 1) / 2 : 0);  // six vectors + index set
   plan->g32_off = 0;
   if (variant == 2) {  // fp32 copy of the packed Gram at the slot's end (relaxed Lanczos steps)
     plan->stride = (plan->stride + 31) / 32 * 32;
@@ -482,7 +504,8 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.gram_doubles = plan.gram_doubles;
     pp.scratch = *ln.scratch;
     pp.scratch_stride = plan.stride;
-    pp.part_global = plan.variant == 4 ? 1 : 0;
+    pp.part_global = plan.variant == 4 || plan.variant == 6 ? 1 : 0;
+    pp.vec_global = plan.variant == 6 ? 1 : 0;
 #ifndef NR_ORDER
 #define NR_ORDER 0  // tuning: 0 the cache-budget rule, 1 always module-major, 2 always permutation-major
 #endif
@@ -670,14 +693,24 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
 // with {corr, net} as {corr, net}, {gram, net^T} per element, so that a packed
 // profile item reads its network values and its Gram entries in one 32-byte
 // gather per pair instead of a separate network launch plus a per-item
-// matrix-core Gram. Built when most of the present modules' summary-profile
-// work is such items (k <= 320, none above S) and the device has the room
-// (40 bytes per matrix element beside the resident pairs during the build).
-int maybe_build_table(nr_ctx* ctx) {
-  if (ctx->table_checked == ctx->modules_serial) return NR_OK;
-  ctx->table_checked = ctx->modules_serial;
-  if (ctx->pairs_es == 2 || !ctx->d_data || ctx->n_present == 0) return NR_OK;
+// matrix-core Gram.
+//
+// The decision depends on shapes only -- never on free device memory -- so
+// the numerical path of a dataset/module set is fixed (the table path and the
+// per-item matrix-core Gram differ at the 1e-12 level): the table is built
+// when (1) the packed-class segment (modules of <= 320 nodes) would be ONE
+// fused launch of the packed kernel, i.e. launch_profiles' own rule: its
+// plan is variant 2 (not the small class, min(k, S) > 112) and none of its
+// modules has more nodes than samples; (2) that segment carries at least
+// half of the present modules' Gram work; (3) n^2 fits kTableMaxElems (the
+// build holds 56 bytes per matrix element: pairs, X^T X and the table). A
+// failed allocation is NR_ERR_OOM, not a silent switch to the other path.
+constexpr int64_t kTableMaxElems = (int64_t)50000 * 50000;  // n <= 50,000: 140 GB during the build
+
+bool table_wanted(nr_ctx* ctx) {
+  if (!ctx->d_data || ctx->n_present == 0) return false;
   const int64_t S = ctx->n_samples, n = ctx->n_nodes;
+  if (n * n > kTableMaxElems) return false;
   double packed_w = 0.0, total_w = 0.0;
   int32_t packed_max = 0;
   for (const int32_t k : ctx->order_k_h) {
@@ -689,11 +722,19 @@ int maybe_build_table(nr_ctx* ctx) {
       packed_max = std::max(packed_max, k);
     }
   }
-  if (packed_max > S || packed_w < 0.5 * total_w) return NR_OK;
-  size_t free_b = 0, total_b = 0;
-  NR_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+  if (packed_max == 0 || packed_max > S || packed_w < 0.5 * total_w) return false;
+  ProfilePlan plan;
+  if (plan_profile(ctx, 1, packed_max, (int)S, &plan) != NR_OK) return false;
+  return plan.variant == 2 &&
+         nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
+}
+
+int maybe_build_table(nr_ctx* ctx) {
+  if (ctx->table_checked == ctx->modules_serial) return NR_OK;
+  ctx->table_checked = ctx->modules_serial;
+  if (ctx->pairs_es == 2 || !table_wanted(ctx)) return NR_OK;
+  const int64_t S = ctx->n_samples, n = ctx->n_nodes;
   const size_t nn = (size_t)n * (size_t)n;
-  if (free_b < nn * 40 + ((size_t)1 << 30)) return NR_OK;
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->obs_stream) NR_HIP(ctx, hipStreamSynchronize(ctx->obs_stream));
   const auto t_build = std::chrono::steady_clock::now();
@@ -709,8 +750,12 @@ int maybe_build_table(nr_ctx* ctx) {
       hipMalloc((void**)&tab, 2 * nn * sizeof(double2)) != hipSuccess ||
       hipMalloc((void**)&cs, (size_t)n * sizeof(double)) != hipSuccess) {
     drop();
-    (void)hipGetLastError();  // no room after all: the per-item Gram path
-    return NR_OK;
+    (void)hipGetLastError();
+    ctx->table_checked = -1;  // a later call tries again
+    return fail(ctx, NR_ERR_OOM,
+                "Gram table allocation failed: " + std::to_string((nn * 40) >> 20) +
+                    " MiB beside the resident matrices (40 bytes per matrix element; the table path is chosen "
+                    "from the shapes, DESIGN.md section 5.2)");
   }
   hipError_t e = nr::launch_gram_full(ctx->d_data, S, n, gram, cs, ctx->stream);
   if (e == hipSuccess) e = nr::launch_widen_pairs(ctx->d_pairs, gram, tab, n, ctx->symmetric, ctx->stream);
@@ -865,9 +910,8 @@ int run_impl(nr_ctx* ctx, int64_t b, int64_t e, uint64_t seed, const uint32_t* p
       } else {
         rc = ensure(ctx, ctx->d_pi, ctx->pi_cap, (size_t)(np * ctx->n_null));
         if (rc) return rc;
-        NR_HIP(ctx, hipMemcpyAsync(ctx->d_pi, pi + (p0 - b) * ctx->n_null,
-                                   (size_t)(np * ctx->n_null) * sizeof(uint32_t),
-                                   hipMemcpyHostToDevice, ctx->stream));
+        NR_HIP(ctx, h2d_async(ctx->d_pi, pi + (p0 - b) * ctx->n_null,
+                              (size_t)(np * ctx->n_null) * sizeof(uint32_t), ctx->stream));
         d_pi = ctx->d_pi;
       }
     }
@@ -933,6 +977,7 @@ int nr_ctx_create(int device, nr_ctx** out) {
   }
   nr_ctx* ctx = new nr_ctx();
   ctx->device = device;
+  ctx->host_threads = g_host_threads.load();
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&ctx->ev[i]);
@@ -992,19 +1037,30 @@ const char* nr_last_error(const nr_ctx* ctx) {
   return ctx ? ctx->err.c_str() : g_create_error.c_str();
 }
 
-// Host threads of the staging copies (nr_set_host_threads; the reference
-// interface passes nCores).
-static std::atomic<int> g_host_threads{8};
-
+// Default host threads of the staging copies for contexts created later
+// (process-wide); a context's own count is nr_ctx_set_host_threads (the
+// reference-interface calls set it from nCores on their contexts only).
 int nr_set_host_threads(int n) {
   g_host_threads = n <= 0 ? 8 : std::min(n, 16);
   return NR_OK;
 }
 
-// Copy n doubles with up to g_host_threads host threads (pageable -> pinned staging).
-static void parallel_copy(double* dst, const double* src, int64_t n) {
+int nr_ctx_set_host_threads(nr_ctx* ctx, int n) {
+  if (!ctx) return NR_ERR_INVALID;
+  ctx->host_threads = n <= 0 ? 8 : std::min(n, 16);
+  return NR_OK;
+}
+
+int nr_h2d_bytes(int64_t* bytes) {
+  if (!bytes) return NR_ERR_INVALID;
+  *bytes = g_h2d_bytes.load();
+  return NR_OK;
+}
+
+// Copy n doubles with up to `threads` host threads (pageable -> pinned staging).
+static void parallel_copy(double* dst, const double* src, int64_t n, int threads) {
   const int64_t min_part = (int64_t)1 << 20;  // 8 MiB per thread at least
-  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(g_host_threads.load(), n / min_part));
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n / min_part));
   if (nt == 1) {
     std::memcpy(dst, src, (size_t)n * sizeof(double));
     return;
@@ -1022,10 +1078,14 @@ static void parallel_copy(double* dst, const double* src, int64_t n) {
 // fill pinned buffer b with chunk i+1 (from the caller's pageable arrays)
 // while the copy engine moves chunk i and, for the corr/net pair, the
 // interleave kernel packs it into the {corr, net} layout. `net` NULL: a plain
-// copy of `corr` into `dst_plain`.
+// copy of `corr` into `dst_plain`. net == corr (NetProps: the network doubles
+// as the unused correlation operand): the matrix crosses PCIe once and fills
+// both halves of the pairs.
 static int upload_pinned(nr_ctx* ctx, const double* corr, const double* net, int64_t n_elem, double2* dst_pairs,
                          double* dst_plain, hipStream_t st) {
-  const int parts = net ? 2 : 1;
+  const bool same = net != nullptr && net == corr;
+  const int parts = net && !same ? 2 : 1;
+  const int threads = ctx->host_threads;
   const int64_t chunk = std::min<int64_t>(n_elem, (int64_t)1 << 23);  // 64 MiB per matrix per chunk
   double* h[2] = {nullptr, nullptr};
   double* d[2] = {nullptr, nullptr};
@@ -1042,13 +1102,14 @@ static int upload_pinned(nr_ctx* ctx, const double* corr, const double* net, int
     const int64_t len = std::min(chunk, n_elem - o);
     if (i >= 2) e = hipEventSynchronize(ev[b]);  // chunk i-2 has left buffer b
     if (e != hipSuccess) break;
-    parallel_copy(h[b], corr + o, len);
-    if (net) parallel_copy(h[b] + chunk, net + o, len);
+    parallel_copy(h[b], corr + o, len, threads);
+    if (parts == 2) parallel_copy(h[b] + chunk, net + o, len, threads);
     if (net) {
-      e = hipMemcpyAsync(d[b], h[b], (size_t)(parts * chunk) * sizeof(double), hipMemcpyHostToDevice, st);
-      if (e == hipSuccess) e = nr::launch_interleave(d[b], d[b] + chunk, dst_pairs + o, len, st);
+      e = h2d_async(d[b], h[b], (size_t)len * sizeof(double), st);
+      if (e == hipSuccess && parts == 2) e = h2d_async(d[b] + chunk, h[b] + chunk, (size_t)len * sizeof(double), st);
+      if (e == hipSuccess) e = nr::launch_interleave(d[b], parts == 2 ? d[b] + chunk : d[b], dst_pairs + o, len, st);
     } else {
-      e = hipMemcpyAsync(dst_plain + o, h[b], (size_t)len * sizeof(double), hipMemcpyHostToDevice, st);
+      e = h2d_async(dst_plain + o, h[b], (size_t)len * sizeof(double), st);
     }
     if (e == hipSuccess) e = hipEventRecord(ev[b], st);
   }
@@ -1064,19 +1125,25 @@ static int upload_pinned(nr_ctx* ctx, const double* corr, const double* net, int
 
 namespace {
 int set_dataset_impl(nr_ctx* ctx, const double* corr, const double* net, const double* data,
-                     int64_t n_nodes, int64_t n_samples, int where);
+                     int64_t n_nodes, int64_t n_samples, int where, int flags);
 }
 
 int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const double* data,
                    int64_t n_nodes, int64_t n_samples, int where) {
+  return nr_set_dataset_ex(ctx, corr, net, data, n_nodes, n_samples, where, 0);
+}
+
+int nr_set_dataset_ex(nr_ctx* ctx, const double* corr, const double* net, const double* data,
+                      int64_t n_nodes, int64_t n_samples, int where, int flags) {
   if (!ctx) return NR_ERR_INVALID;
+  if (flags & ~NR_SCALE_DATA) return fail(ctx, NR_ERR_INVALID, "unknown nr_set_dataset_ex flags");
   if (!corr || !net || n_nodes <= 0) return fail(ctx, NR_ERR_INVALID, "corr/net missing or n_nodes <= 0");
   if (data && n_samples < 2) return fail(ctx, NR_ERR_INVALID, "data needs n_samples >= 2");
   if (n_nodes > (int64_t)INT32_MAX) return fail(ctx, NR_ERR_UNSUPPORTED, "n_nodes exceeds 2^31-1");
   NR_HIP(ctx, hipSetDevice(ctx->device));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   reset_dataset(ctx);
-  const int rc = set_dataset_impl(ctx, corr, net, data, n_nodes, n_samples, where);
+  const int rc = set_dataset_impl(ctx, corr, net, data, n_nodes, n_samples, where, flags);
   if (rc != NR_OK) {
     (void)hipStreamSynchronize(ctx->stream);
     reset_dataset(ctx);
@@ -1086,7 +1153,7 @@ int nr_set_dataset(nr_ctx* ctx, const double* corr, const double* net, const dou
 
 namespace {
 int set_dataset_impl(nr_ctx* ctx, const double* corr, const double* net, const double* data,
-                     int64_t n_nodes, int64_t n_samples, int where) {
+                     int64_t n_nodes, int64_t n_samples, int where, int flags) {
   const int64_t n_elem = n_nodes * n_nodes;
   NR_HIP(ctx, hipMalloc((void**)&ctx->d_pairs, (size_t)n_elem * sizeof(double2)));
   if (where == NR_DEVICE) {
@@ -1103,12 +1170,25 @@ int set_dataset_impl(nr_ctx* ctx, const double* corr, const double* net, const d
     const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
     NR_HIP(ctx, hipMalloc((void**)&ctx->d_data, bytes + 2 * (size_t)n_samples * sizeof(double)));
     if (int rc = fill_virtual_columns(ctx, n_nodes, n_samples)) return rc;
+    // NR_SCALE_DATA: the raw data goes to a device buffer and is scaled there
+    // (Scale, src/scale.cpp:14-25) straight into the resident block
+    double* raw = nullptr;
+    if (flags & NR_SCALE_DATA) NR_HIP(ctx, hipMalloc((void**)&raw, bytes));
+    double* dst = raw ? raw : ctx->d_data;
+    int rc = NR_OK;
     if (where == NR_DEVICE) {
-      NR_HIP(ctx, hipMemcpyAsync(ctx->d_data, data, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+      const hipError_t e = hipMemcpyAsync(dst, data, bytes, hipMemcpyDeviceToDevice, ctx->stream);
+      if (e != hipSuccess) rc = hip_fail(ctx, e, "data copy");
     } else {
-      const int rc = upload_pinned(ctx, data, nullptr, n_samples * n_nodes, nullptr, ctx->d_data, ctx->stream);
-      if (rc) return rc;
+      rc = upload_pinned(ctx, data, nullptr, n_samples * n_nodes, nullptr, dst, ctx->stream);
     }
+    if (!rc && raw) {
+      hipError_t e = nr::launch_scale(raw, ctx->d_data, n_samples, n_nodes, ctx->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+      if (e != hipSuccess) rc = hip_fail(ctx, e, "scale");
+    }
+    if (raw) (void)hipFree(raw);
+    if (rc) return rc;
   }
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->symmetric = (asym & 1) ? 0 : 1;
@@ -1145,7 +1225,7 @@ static int upload_file_matrix(nr_ctx* ctx, nr::RMatrixReader& rd, double2* pairs
     if (e != hipSuccess) break;
     read_ok = rd.read_raw(h[b], len);
     if (!read_ok) break;
-    e = hipMemcpyAsync(d[b], h[b], (size_t)len * sizeof(double), hipMemcpyHostToDevice, st);
+    e = h2d_async(d[b], h[b], (size_t)len * sizeof(double), st);
     if (e == hipSuccess) e = nr::launch_xdr(d[b], pairs ? pairs + o : nullptr, half, plain ? plain + o : nullptr, len, st);
     if (e == hipSuccess) e = hipEventRecord(ev[b], st);
   }
@@ -1309,6 +1389,137 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   dst->symmetric = src->symmetric;
   dst->corr_finite = src->corr_finite;
   dst->net_finite = src->net_finite;
+  return NR_OK;
+}
+
+// One resident dataset to n - 1 other contexts ("broadcast once
+// per test dataset"), bandwidth-optimal on a full xGMI mesh: a scatter and an
+// all-gather of peer copies. Each buffer is cut into n - 1 pieces. Phase 1:
+// piece p goes from the source to context p + 1 (every source link busy at
+// once, B / (n-1) bytes each). Phase 2: context p + 1 forwards piece p to the
+// other n - 2 destinations over its own direct links, each copy behind the
+// event that marks the piece's arrival. Every link carries at most
+// B / (n-1) per phase: 2B / ((n-1) L) in all, against B / L for a direct
+// fan-out (each destination pulls all B over its one link to the source) or
+// a single pipelined ring (DESIGN.md section 7 has the arithmetic). The source
+// must be idle; on failure every destination is left with no dataset.
+int nr_broadcast_dataset(nr_ctx* const* ctxs, int n) {
+  if (!ctxs || n < 1) return NR_ERR_INVALID;
+  nr_ctx* src = ctxs[0];
+  if (!src) return NR_ERR_INVALID;
+  for (int g = 1; g < n; ++g)
+    for (int h = 0; h < g; ++h)
+      if (!ctxs[g] || ctxs[g] == ctxs[h]) return fail(src, NR_ERR_INVALID, "broadcast: contexts must be distinct");
+  if (!src->d_pairs) return fail(src, NR_ERR_INVALID, "source context has no dataset");
+  if (n == 1) return NR_OK;
+  const int parts = n - 1;
+  struct Buf {
+    const char* s;
+    std::vector<char*> d;
+    size_t bytes;
+  };
+  std::vector<Buf> bufs;
+  const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2) * (size_t)src->pairs_es;
+  const size_t data_bytes = (size_t)(src->n_samples * (src->n_nodes + 2)) * sizeof(double);  // + virtual columns
+  const size_t cs_bytes = (size_t)src->n_nodes * sizeof(double);
+  bufs.push_back({reinterpret_cast<const char*>(src->d_pairs), std::vector<char*>(n, nullptr), pair_bytes});
+  if (src->d_data) bufs.push_back({reinterpret_cast<const char*>(src->d_data), std::vector<char*>(n, nullptr), data_bytes});
+  if (src->d_colsum)
+    bufs.push_back({reinterpret_cast<const char*>(src->d_colsum), std::vector<char*>(n, nullptr), cs_bytes});
+  auto clear_all = [&]() {
+    for (int g = 1; g < n; ++g) {
+      (void)hipSetDevice(ctxs[g]->device);
+      (void)hipStreamSynchronize(ctxs[g]->stream);
+      reset_dataset(ctxs[g]);
+    }
+  };
+  for (int g = 1; g < n; ++g) {
+    nr_ctx* d = ctxs[g];
+    NR_HIP(d, hipSetDevice(d->device));
+    NR_HIP(d, hipStreamSynchronize(d->stream));
+    reset_dataset(d);
+    hipError_t e = hipMalloc((void**)&d->d_pairs, pair_bytes);
+    if (e == hipSuccess && src->d_data) e = hipMalloc((void**)&d->d_data, data_bytes);
+    if (e == hipSuccess && src->d_colsum) e = hipMalloc((void**)&d->d_colsum, cs_bytes);
+    if (e != hipSuccess) {
+      const int rc = hip_fail(d, e, "broadcast allocation");
+      clear_all();
+      return fail(src, rc, d->err);
+    }
+    size_t b = 0;
+    bufs[b++].d[g] = reinterpret_cast<char*>(d->d_pairs);
+    if (src->d_data) bufs[b++].d[g] = reinterpret_cast<char*>(d->d_data);
+    if (src->d_colsum) bufs[b++].d[g] = reinterpret_cast<char*>(d->d_colsum);
+  }
+  auto piece = [&](size_t bytes, int p, size_t* a, size_t* len) {
+    const size_t per = ((bytes + parts - 1) / parts + 255) / 256 * 256;
+    *a = std::min(bytes, (size_t)p * per);
+    *len = std::min(bytes, *a + per) - *a;
+  };
+  NR_HIP(src, hipSetDevice(src->device));
+  NR_HIP(src, hipStreamSynchronize(src->stream));
+  std::vector<hipEvent_t> ev(parts, nullptr);
+  hipError_t e = hipSuccess;
+  // phase 1: the scatter
+  for (int p = 0; p < parts && e == hipSuccess; ++p) {
+    nr_ctx* d = ctxs[p + 1];
+    e = hipSetDevice(d->device);
+    for (const Buf& bf : bufs) {
+      size_t a, len;
+      piece(bf.bytes, p, &a, &len);
+      if (e == hipSuccess && len)
+        e = hipMemcpyPeerAsync(bf.d[p + 1] + a, d->device, bf.s + a, src->device, len, d->stream);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[p], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev[p], d->stream);
+  }
+  // phase 2: the all-gather among the destinations
+  for (int g = 1; g < n && e == hipSuccess; ++g) {
+    nr_ctx* d = ctxs[g];
+    e = hipSetDevice(d->device);
+    for (int p = 0; p < parts && e == hipSuccess; ++p) {
+      if (p == g - 1) continue;
+      e = hipStreamWaitEvent(d->stream, ev[p], 0);
+      for (const Buf& bf : bufs) {
+        size_t a, len;
+        piece(bf.bytes, p, &a, &len);
+        if (e == hipSuccess && len)
+          e = hipMemcpyPeerAsync(bf.d[g] + a, d->device, bf.d[p + 1] + a, ctxs[p + 1]->device, len, d->stream);
+      }
+    }
+  }
+  for (int g = 1; g < n; ++g) {
+    const hipError_t e2 = hipSetDevice(ctxs[g]->device);
+    const hipError_t e3 = hipStreamSynchronize(ctxs[g]->stream);
+    if (e == hipSuccess) e = e2 != hipSuccess ? e2 : e3;
+  }
+  for (hipEvent_t x : ev)
+    if (x) (void)hipEventDestroy(x);
+  if (e != hipSuccess) {
+    const int rc = hip_fail(src, e, "dataset broadcast");
+    clear_all();
+    return rc;
+  }
+  for (int g = 1; g < n; ++g) {
+    nr_ctx* d = ctxs[g];
+    d->pairs_es = src->pairs_es;
+    d->n_nodes = src->n_nodes;
+    d->n_samples = src->n_samples;
+    d->node_names = src->node_names;
+    d->symmetric = src->symmetric;
+    d->corr_finite = src->corr_finite;
+    d->net_finite = src->net_finite;
+    d->table_ms = src->table_ms;
+  }
+  (void)hipSetDevice(src->device);
+  return NR_OK;
+}
+
+int nr_clear_dataset(nr_ctx* ctx) {
+  if (!ctx) return NR_ERR_INVALID;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  reset_dataset(ctx);
   return NR_OK;
 }
 
@@ -1623,7 +1834,7 @@ int nr_scale(nr_ctx* ctx, const double* data, int64_t n_samples, int64_t n_nodes
   double *din = nullptr, *dout = nullptr;
   NR_HIP(ctx, hipMalloc((void**)&din, bytes));
   hipError_t e = hipMalloc((void**)&dout, bytes);
-  if (e == hipSuccess) e = hipMemcpyAsync(din, data, bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = h2d_async(din, data, bytes, ctx->stream);
   if (e == hipSuccess) e = nr::launch_scale(din, dout, n_samples, n_nodes, ctx->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(scaled, dout, bytes, hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -1644,7 +1855,7 @@ int nr_check_finite(nr_ctx* ctx, const double* mat, int64_t n_elem, int* all_fin
   hipError_t e = hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream);
   for (int64_t o = 0; o < n_elem && e == hipSuccess; o += chunk) {
     const int64_t len = std::min(chunk, n_elem - o);
-    e = hipMemcpyAsync(d, mat + o, (size_t)len * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
+    e = h2d_async(d, mat + o, (size_t)len * sizeof(double), ctx->stream);
     if (e == hipSuccess) e = nr::launch_finite(d, len, ctx->d_counters + 5, ctx->stream);
   }
   int bad = 0;

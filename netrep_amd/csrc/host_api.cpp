@@ -77,13 +77,116 @@ struct CtxDeleter {
 };
 typedef std::unique_ptr<nr_ctx, CtxDeleter> CtxPtr;
 
+// Contexts are pooled across calls (streams, events, slot scratch and
+// staging buffers survive; the dataset does not): modulePreservation makes
+// one PermutationProcedure call per (discovery, test) pair.
+std::mutex g_pool_mu;
+struct Pooled {
+  int device;
+  CtxPtr ctx;
+};
+// at process exit the pooled contexts are left to the driver's teardown (the
+// HIP runtime may already be gone), as the prefetch contexts are
+struct Pool {
+  std::vector<Pooled> v;
+  ~Pool() {
+    for (Pooled& p : v) (void)p.ctx.release();
+  }
+};
+Pool g_pool_;
+std::vector<Pooled>& g_pool = g_pool_.v;
+std::unordered_map<const nr_ctx*, int> g_ctx_device;  // device of every context this layer opened
+constexpr size_t kPoolMax = 8;
+
 int open_ctx(int device, CtxPtr& out) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); ++i) {
+      if (g_pool[i].device == device) {
+        out = std::move(g_pool[i].ctx);
+        g_pool.erase(g_pool.begin() + (long)i);
+        return NR_OK;
+      }
+    }
+  }
   nr_ctx* c = nullptr;
   const int rc = nr_ctx_create(device, &c);
   if (rc) return set_err(rc, nr_last_error(nullptr));
   out.reset(c);
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_ctx_device[c] = device;
   return NR_OK;
 }
+
+// Back to the pool without its dataset (HBM is not held between calls).
+void give_ctx(CtxPtr& c) {
+  if (!c) return;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  auto it = g_ctx_device.find(c.get());
+  if (it == g_ctx_device.end() || g_pool.size() >= kPoolMax || nr_clear_dataset(c.get()) != NR_OK) {
+    if (it != g_ctx_device.end()) g_ctx_device.erase(it);
+    c.reset();
+    return;
+  }
+  g_pool.push_back({it->second, std::move(c)});
+}
+
+// Returns every context of a call to the pool when it goes out of scope.
+struct CtxLease {
+  std::vector<CtxPtr>* v;
+  ~CtxLease() {
+    for (CtxPtr& c : *v) give_ctx(c);
+  }
+};
+
+// A dataset kept resident between calls that name the same host arrays: the
+// pointers and shape must match, and so must a fingerprint of 1,024 sampled
+// elements of each array (evenly spread, both ends included) -- a freed and
+// reused address with other contents is not mistaken for the same matrix.
+uint64_t fingerprint(const double* a, int64_t n) {
+  uint64_t h = 0x243F6A8885A308D3ull ^ (uint64_t)n;
+  if (!a || n <= 0) return h;
+  const int64_t k = std::min<int64_t>(n, 1024);
+  for (int64_t i = 0; i < k; ++i) {
+    const int64_t pos = k > 1 ? i * (n - 1) / (k - 1) : 0;
+    uint64_t b;
+    std::memcpy(&b, a + pos, 8);
+    h ^= b + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  }
+  return h;
+}
+
+struct Resident {
+  CtxPtr ctx;
+  const double *data = nullptr, *corr = nullptr, *net = nullptr;
+  int64_t n_samples = 0, n_nodes = 0;
+  uint64_t fp = 0;
+  static uint64_t fp_of(const double* data, const double* corr, const double* net, int64_t s, int64_t n) {
+    return fingerprint(corr, n * n) * 3 + fingerprint(net, n * n) * 5 + fingerprint(data, s * n) * 7;
+  }
+  bool holds(const double* d, const double* c, const double* nt, int64_t s, int64_t n) const {
+    return ctx && data == d && corr == c && net == nt && n_nodes == n && (d == nullptr || n_samples == s) &&
+           fp == fp_of(d, c, nt, d ? s : 0, n);
+  }
+  void keep(CtxPtr c, const double* d, const double* cr, const double* nt, int64_t s, int64_t n) {
+    ctx = std::move(c);
+    data = d;
+    corr = cr;
+    net = nt;
+    n_samples = d ? s : 0;
+    n_nodes = n;
+    fp = fp_of(d, cr, nt, n_samples, n);
+  }
+  void drop() {
+    give_ctx(ctx);
+    data = corr = net = nullptr;
+    n_samples = n_nodes = 0;
+  }
+  ~Resident() { (void)ctx.release(); }  // process exit: as Pool
+};
+std::mutex g_res_mu;
+Resident g_disc_res;   // netrep_IntermediateProperties' discovery dataset
+Resident g_props_res;  // netrep_NetProps' dataset (net + data scaled on the device)
 
 // Contexts requested by NETREP_NUM_GPUS, clamped to the visible GPUs unless
 // NETREP_SHARE_DEVICE=1 (test mode: contexts share GPUs round-robin, so the
@@ -156,7 +259,7 @@ std::vector<std::unique_ptr<Prefetch>> g_pf;
 
 void drop_prefetch(std::unique_ptr<Prefetch>& p) {
   p->join();
-  p->ctx.reset();  // context destroyed while the runtime is alive
+  give_ctx(p->ctx);  // back to the pool (its dataset freed) while the runtime is alive
   p.reset();
 }
 
@@ -233,6 +336,22 @@ int netrep_format_progress(int64_t done, int64_t total, char* buf, int64_t cap) 
   return (n < 0 || n >= cap) ? -1 : n;
 }
 
+void netrep_ReleaseResident(void) {
+  netrep_DiscardPrefetch();
+  {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    g_disc_res.drop();
+    g_props_res.drop();
+  }
+  std::vector<Pooled> all;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    all.swap(g_pool);
+    for (Pooled& p : all) g_ctx_device.erase(p.ctx.get());
+  }
+  all.clear();  // contexts destroyed while the runtime is alive
+}
+
 void netrep_DiscardPrefetch(void) {
   std::vector<std::unique_ptr<Prefetch>> all;
   {
@@ -287,7 +406,8 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
                      const char* const* t_names, const char* const* ma_names, const char* const* ma_labels,
                      int64_t n_assign, const char* const* modules, int64_t n_modules, int64_t n_perm,
                      const char* null_hypothesis, int32_t verbose, uint64_t seed, const uint32_t* pi,
-                     double* nulls_out, double* observed_out, CtxPtr preloaded, int64_t pi_len = -1) {
+                     double* nulls_out, double* observed_out, CtxPtr preloaded, int32_t n_cores,
+                     int64_t pi_len = -1) {
   if (with_data && !disc->contribution)
     return set_err(NR_ERR_INVALID, "discProps has no 'contribution' but tData was given");
   const std::string null_type = null_hypothesis ? null_hypothesis : "overlap";
@@ -360,6 +480,7 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
   int n_dev = 1;
   const int n_gpu = (n_perm > 0) ? (int)std::min<int64_t>(gpu_count_requested(&n_dev), std::max<int64_t>(n_perm, 1)) : 1;
   std::vector<CtxPtr> ctxs(n_gpu);
+  CtxLease lease{&ctxs};  // the contexts go back to the pool (without the dataset) on every return
   // a dataset already resident (prefetched or loaded from files) becomes GPU 0's
   ctxs[0] = std::move(preloaded);
   const bool prefetched = ctxs[0] != nullptr;
@@ -367,25 +488,33 @@ int permutation_impl(const netrep_disc_props* disc, bool with_data, const double
     int rc = open_ctx(g % n_dev, ctxs[g]);
     if (rc) return rc;
   }
+  for (CtxPtr& c : ctxs) nr_ctx_set_host_threads(c.get(), n_cores);  // nThreads: this call's host threads
   // The host matrices cross PCIe once, into the first GPU; the other GPUs
-  // receive them device to device over xGMI (nr_copy_dataset), concurrently.
+  // receive them device to device by the scatter + all-gather broadcast over
+  // the xGMI mesh (nr_broadcast_dataset).
+  if (!prefetched) {
+    const int rc = nr_set_dataset(ctxs[0].get(), t_corr, t_net, t_data, n_nodes, n_samples, NR_HOST);
+    if (rc) return ctx_err(rc, ctxs[0].get());
+  }
+  if (n_gpu > 1) {
+    std::vector<nr_ctx*> raw(n_gpu);
+    for (int g = 0; g < n_gpu; ++g) raw[g] = ctxs[g].get();
+    const int rc = nr_broadcast_dataset(raw.data(), n_gpu);
+    if (rc) return ctx_err(rc, ctxs[0].get());
+  }
   std::vector<int> rcs(n_gpu, NR_OK);
   auto setup = [&](int g) {
     nr_ctx* c = ctxs[g].get();
-    int rc = g > 0 ? nr_copy_dataset(c, ctxs[0].get())
-                   : prefetched ? NR_OK : nr_set_dataset(c, t_corr, t_net, t_data, n_nodes, n_samples, NR_HOST);
-    if (!rc)
-      rc = nr_set_modules(c, ms.n_rows, ms.n_present, ms.row_of.data(), ms.node_off.data(),
-                          ms.test_idx.data(), ms.null_pos.data(), ms.disc_cv.data(),
-                          ms.disc_wd.data(), with_data ? ms.disc_nc.data() : nullptr);
+    int rc = nr_set_modules(c, ms.n_rows, ms.n_present, ms.row_of.data(), ms.node_off.data(),
+                            ms.test_idx.data(), ms.null_pos.data(), ms.disc_cv.data(),
+                            ms.disc_wd.data(), with_data ? ms.disc_nc.data() : nullptr);
     if (!rc && !ms.null_idx.empty()) rc = nr_set_null_pool(c, ms.null_idx.data(), (int64_t)ms.null_idx.size());
     rcs[g] = rc;
   };
-  setup(0);
-  if (rcs[0]) return ctx_err(rcs[0], ctxs[0].get());
   {
     std::vector<std::thread> th;
     for (int g = 1; g < n_gpu; ++g) th.emplace_back(setup, g);
+    setup(0);
     for (auto& t : th) t.join();
   }
   for (int g = 0; g < n_gpu; ++g)
@@ -476,7 +605,6 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
                                 int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
                                 int32_t verbose, uint64_t seed, const uint32_t* pi,
                                 double* nulls_out, double* observed_out) try {
-  nr_set_host_threads(n_cores);  // nThreads bounds the host threads of the call
   if (!disc || !t_corr || !t_net || !t_names || !ma_names || !ma_labels || !modules ||
       !observed_out || n_perm < 0 || (n_perm > 0 && !nulls_out) || n_nodes <= 0)
     return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedure");
@@ -484,7 +612,7 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
   CtxPtr pre = take_prefetch(t_data, t_corr, t_net, n_samples, n_nodes);
   return permutation_impl(disc, t_data != nullptr, t_data, t_corr, t_net, n_samples, n_nodes, t_names, ma_names,
                           ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose, seed, pi,
-                          nulls_out, observed_out, std::move(pre));
+                          nulls_out, observed_out, std::move(pre), n_cores);
 } catch (const std::bad_alloc&) {
   return set_err(NR_ERR_OOM, "host memory allocation failed");
 } catch (const std::exception& e) {
@@ -498,16 +626,21 @@ int netrep_PermutationProcedureFiles(const netrep_disc_props* disc, const char* 
                                      int64_t n_perm, int32_t n_cores, const char* null_hypothesis,
                                      int32_t verbose, uint64_t seed, const uint32_t* pi, int64_t pi_len,
                                      double* nulls_out, double* observed_out) try {
-  nr_set_host_threads(n_cores);  // nThreads bounds the host threads of the call
   if (!disc || !t_corr_file || !t_net_file || !ma_names || !ma_labels || !modules || !observed_out ||
       n_perm < 0 || (n_perm > 0 && !nulls_out))
     return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedureFiles");
   CtxPtr ctx;
   int rc = open_ctx(0, ctx);
   if (rc) return rc;
+  std::vector<CtxPtr> lease_v;
+  CtxLease lease{&lease_v};  // back to the pool if the load fails
   // disk.matrix files straight to HBM; tData scaled on the device
   rc = nr_set_dataset_files(ctx.get(), t_corr_file, t_net_file, t_data_file, nullptr, nullptr, nullptr, 1);
-  if (rc) return ctx_err(rc, ctx.get());
+  if (rc) {
+    rc = ctx_err(rc, ctx.get());
+    lease_v.push_back(std::move(ctx));
+    return rc;
+  }
   int64_t n_nodes = 0, n_samples = 0, need = 0;
   nr_dataset_shape(ctx.get(), &n_nodes, &n_samples);
   nr_dataset_colnames(ctx.get(), nullptr, 0, &need);
@@ -519,7 +652,7 @@ int netrep_PermutationProcedureFiles(const netrep_disc_props* disc, const char* 
     return set_err(NR_ERR_INVALID, "the network file has no column names (node names are needed)");
   return permutation_impl(disc, t_data_file != nullptr, nullptr, nullptr, nullptr, n_samples, n_nodes, names.data(),
                           ma_names, ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose,
-                          seed, pi, nulls_out, observed_out, std::move(ctx), pi_len);
+                          seed, pi, nulls_out, observed_out, std::move(ctx), n_cores, pi_len);
 } catch (const std::bad_alloc&) {
   return set_err(NR_ERR_OOM, "host memory allocation failed");
 } catch (const std::exception& e) {
@@ -589,11 +722,21 @@ int netrep_IntermediateProperties(const double* d_data, const double* d_corr, co
   }
   const int32_t n_mod = (int32_t)which.size();
   if (n_mod == 0) return NR_OK;
-  CtxPtr ctx;
-  int rc = open_ctx(0, ctx);
-  if (rc) return rc;
-  rc = nr_set_dataset(ctx.get(), d_corr, d_net, d_data, n_nodes, n_samples, NR_HOST);
-  if (rc) return ctx_err(rc, ctx.get());
+  // The discovery dataset stays resident across the calls of one discovery
+  // dataset's loop over test datasets (the reference loads it once per di,
+  // R/modulePreservation.R:553-590): uploaded only when these arrays are not
+  // the resident ones.
+  std::lock_guard<std::mutex> res_lk(g_res_mu);
+  int rc = NR_OK;
+  if (!g_disc_res.holds(d_data, d_corr, d_net, n_samples, n_nodes)) {
+    g_disc_res.drop();
+    CtxPtr ctx;
+    if ((rc = open_ctx(0, ctx))) return rc;
+    rc = nr_set_dataset(ctx.get(), d_corr, d_net, d_data, n_nodes, n_samples, NR_HOST);
+    if (rc) return ctx_err(rc, ctx.get());
+    g_disc_res.keep(std::move(ctx), d_data, d_corr, d_net, n_samples, n_nodes);
+  }
+  nr_ctx* const ctx = g_disc_res.ctx.get();
   const int64_t nodes = node_off.back();
   int64_t n_cv = 0;
   for (int32_t m = 0; m < n_mod; ++m) {
@@ -601,9 +744,9 @@ int netrep_IntermediateProperties(const double* d_data, const double* d_corr, co
     n_cv += k * (k - 1) / 2;
   }
   std::vector<double> cv((size_t)std::max<int64_t>(n_cv, 1)), wd((size_t)nodes), nc(with_data ? (size_t)nodes : 0);
-  rc = nr_module_vectors(ctx.get(), n_mod, node_off.data(), idx.data(), cv.data(), wd.data(), nullptr,
+  rc = nr_module_vectors(ctx, n_mod, node_off.data(), idx.data(), cv.data(), wd.data(), nullptr,
                          with_data ? nc.data() : nullptr, nullptr, nullptr);
-  if (rc) return ctx_err(rc, ctx.get());
+  if (rc) return ctx_err(rc, ctx);
   // Concatenate in `modules` order (src/discProps.cpp:119-125).
   int64_t o_cv = 0, o_n = 0;
   for (int32_t m = 0; m < n_mod; ++m) {
@@ -678,19 +821,23 @@ int netrep_NetProps(const double* data, const double* net, int64_t n_samples, in
   }
   const int32_t n_mod = (int32_t)which.size();
   if (n_mod == 0) return NR_OK;
-  CtxPtr ctx;
-  int rc = open_ctx(0, ctx);
-  if (rc) return rc;
-  std::vector<double> scaled;
-  if (with_data) {  // NetProps scales internally (src/properties.cpp:49)
-    scaled.resize((size_t)(n_samples * n_nodes));
-    rc = nr_scale(ctx.get(), data, n_samples, n_nodes, scaled.data());
+  // NetProps scales internally (src/properties.cpp:49): the raw data is
+  // scaled on the device on its way into HBM. No correlation matrix on this
+  // path: the network doubles as the (unused) correlation operand and
+  // crosses PCIe once. The dataset stays resident while later calls name the
+  // same arrays (networkProperties calls NetProps per (discovery, test) pair,
+  // R/networkProperties.R:295-302).
+  std::lock_guard<std::mutex> res_lk(g_res_mu);
+  int rc = NR_OK;
+  if (!g_props_res.holds(data, net, net, n_samples, n_nodes)) {
+    g_props_res.drop();
+    CtxPtr ctx;
+    if ((rc = open_ctx(0, ctx))) return rc;
+    rc = nr_set_dataset_ex(ctx.get(), net, net, data, n_nodes, n_samples, NR_HOST, with_data ? NR_SCALE_DATA : 0);
     if (rc) return ctx_err(rc, ctx.get());
+    g_props_res.keep(std::move(ctx), data, net, net, n_samples, n_nodes);
   }
-  // No correlation matrix on this path: the network doubles as the (unused)
-  // correlation operand of the interleaved dataset.
-  rc = nr_set_dataset(ctx.get(), net, net, with_data ? scaled.data() : nullptr, n_nodes, n_samples, NR_HOST);
-  if (rc) return ctx_err(rc, ctx.get());
+  nr_ctx* const ctx = g_props_res.ctx.get();
   const int64_t nodes = node_off.back();
   std::vector<double> wd((size_t)nodes), aw((size_t)n_mod), nc, sp, coh;
   if (with_data) {
@@ -698,10 +845,10 @@ int netrep_NetProps(const double* data, const double* net, int64_t n_samples, in
     sp.resize((size_t)(n_mod * n_samples));
     coh.resize((size_t)n_mod);
   }
-  rc = nr_module_vectors(ctx.get(), n_mod, node_off.data(), idx.data(), nullptr, wd.data(), aw.data(),
+  rc = nr_module_vectors(ctx, n_mod, node_off.data(), idx.data(), nullptr, wd.data(), aw.data(),
                          with_data ? nc.data() : nullptr, with_data ? sp.data() : nullptr,
                          with_data ? coh.data() : nullptr);
-  if (rc) return ctx_err(rc, ctx.get());
+  if (rc) return ctx_err(rc, ctx);
   auto na_if = [&](double x) { return std::isfinite(x) ? x : na; };
   for (int32_t m = 0; m < n_mod; ++m) {
     const int64_t mi = which[m];
@@ -727,11 +874,12 @@ int netrep_NetProps(const double* data, const double* net, int64_t n_samples, in
 int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes, double* scaled_out) try {
   if (!data || !scaled_out || n_samples <= 0 || n_nodes <= 0)
     return set_err(NR_ERR_INVALID, "invalid arguments to Scale");
-  CtxPtr ctx;
-  int rc = open_ctx(0, ctx);
+  std::vector<CtxPtr> v(1);
+  CtxLease lease{&v};
+  int rc = open_ctx(0, v[0]);
   if (rc) return rc;
-  rc = nr_scale(ctx.get(), data, n_samples, n_nodes, scaled_out);
-  if (rc) return ctx_err(rc, ctx.get());
+  rc = nr_scale(v[0].get(), data, n_samples, n_nodes, scaled_out);
+  if (rc) return ctx_err(rc, v[0].get());
   return NR_OK;
 } catch (const std::bad_alloc&) {
   return set_err(NR_ERR_OOM, "host memory allocation failed");
@@ -741,12 +889,13 @@ int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes, double*
 
 int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol) try {
   if (!mat || nrow < 0 || ncol < 0) return set_err(NR_ERR_INVALID, "invalid arguments to CheckFinite");
-  CtxPtr ctx;
-  int rc = open_ctx(0, ctx);
+  std::vector<CtxPtr> v(1);
+  CtxLease lease{&v};
+  int rc = open_ctx(0, v[0]);
   if (rc) return rc;
   int ok = 1;
-  rc = nr_check_finite(ctx.get(), mat, nrow * ncol, &ok);
-  if (rc) return ctx_err(rc, ctx.get());
+  rc = nr_check_finite(v[0].get(), mat, nrow * ncol, &ok);
+  if (rc) return ctx_err(rc, v[0].get());
   if (!ok) return set_err(NR_ERR_NONFINITE, "matrices cannot have non-finite or missing values");
   return NR_OK;
 } catch (const std::bad_alloc&) {

@@ -98,6 +98,8 @@ struct ProfileParams {
   int64_t basis_doubles;       // Lanczos basis doubles per slot (behind the Gram)
   int64_t g32_off;             // doubles from the slot start to the fp32 copy of the packed Gram
                                // (relaxed Lanczos steps; 0: no copy, fp64 matvecs throughout)
+  int32_t vec_global;          // 1: the Lanczos vectors, per-node arrays and index set in the slot's
+                               // scratch too (Lanczos dimensions beyond the LDS vectors: variant 6)
   int32_t order_tail;          // queue order: 0 = module-major (large modules first); T > 0 =
                                // permutation-major over all modules (a size mix in flight) for the
                                // first n_perm - T permutations, the last T module-major
@@ -139,7 +141,7 @@ hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* ou
 size_t profile_small_lds();
 int profile_small_per_cu();
 // variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch,
-// 5 the small class
+// 5 the small class, 6 full Gram with the partials and every vector in scratch
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);
 hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,

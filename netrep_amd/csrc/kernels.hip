@@ -1662,11 +1662,15 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   // packed: one partial array per wave, which also serves as the Ritz checks'
   // work area (twork, 5 mmax doubles) between matvecs
   const int64_t n_part = PACKED ? packed_part_doubles(NW, kmax, mmax) : (int64_t)NW * kmax;
-  const LzLds L = carve_lds<NW>(smem, kmax, mmax, pglob ? 0 : n_part, &part, PACKED);
-  const int tid = threadIdx.x;
   double* G = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;  // Gram
   const int ld = P.ld;
   double* Q = G + P.gram_doubles;                                  // Lanczos basis
+  // variant 6: every vector in the slot's scratch behind the partials
+  const bool vglob = !PACKED && P.vec_global;
+  part = nullptr;
+  const LzLds L = vglob ? carve_split<NW>(smem, Q + P.basis_doubles + (int64_t)NW * kmax, kmax, mmax)
+                        : carve_lds<NW>(smem, kmax, mmax, pglob ? 0 : n_part, &part, PACKED);
+  const int tid = threadIdx.x;
   // fp32 copy of the packed Gram for the relaxed Lanczos steps (0: off)
   float* G32 = PACKED && P.g32_off > 0 ? reinterpret_cast<float*>(G + P.g32_off) : nullptr;
   if (pglob) part = Q + P.basis_doubles;
@@ -2067,6 +2071,8 @@ int profile_kvec_max(int m_max) {
 
 size_t profile_kernel_lds(int k_max, int m_max, int n_samples, int variant) {
   (void)n_samples;
+  if (variant == 6)  // reduction scratch + tridiagonal arrays only (carve_split)
+    return sizeof(double) * (8 * NR_WAVES + 12 * (size_t)m_max + 3);
   if (variant == 4)  // full Gram, matvec partials in global scratch
     return sizeof(double) * (8 * NR_WAVES + 6 * (size_t)k_max + 12 * (size_t)m_max + 3) + sizeof(uint32_t) * k_max;
   const bool packed = variant != 0;

@@ -25,6 +25,12 @@ def _ptr(a, ctype=C.c_double):
     return a.ctypes.data_as(C.POINTER(ctype))
 
 
+# The 16 phase-stamp slots as include/netrep_gpu.h (nr_set_stamps) lists them.
+STAMP_SLOTS = ["index", "gram", "lanczos_setup", "matvec", "three_term_omega", "statistics", "q_update",
+               "ritz_checks", "start_column", "reorth", "ritz_vector", "node_contributions", "ritz_coefficients",
+               "s13", "s14", "s15"]
+
+
 class Engine:
     """One GPU context. ``device`` is the HIP ordinal."""
 
@@ -113,6 +119,18 @@ class Engine:
         self.n_stat = 7 if data_ptr else 4
         self.n_nodes = n_nodes
         self.n_samples = n_samples if data_ptr else 0
+
+    def broadcast_dataset_to(self, others):
+        """This context's resident dataset to every context in `others`
+        (nr_broadcast_dataset: scatter + all-gather of peer copies)."""
+        hs = (C.c_void_p * (1 + len(others)))(self._h.value, *[o._h.value for o in others])
+        self._check(self._lib.nr_broadcast_dataset(hs, 1 + len(others)))
+        for o in others:
+            o.n_stat, o.n_nodes, o.n_samples = self.n_stat, self.n_nodes, self.n_samples
+
+    def set_host_threads(self, n: int):
+        """Host threads of this context's staging copies (nr_ctx_set_host_threads)."""
+        self._check(self._lib.nr_ctx_set_host_threads(self._h, int(n)))
 
     def copy_dataset_from(self, other: "Engine"):
         """Device-to-device copy of another context's resident dataset
@@ -275,8 +293,7 @@ class Engine:
     def stamps(self):
         out = (C.c_uint64 * 16)()
         self._check(self._lib.nr_get_stamps(self._h, out))
-        names = ["index", "gram", "lanczos_init", "lanczos_matvec", "three_term", "stats", "beta_sync", "checks",
-                 "start", "reorth", "ritz_vector", "contrib", "ritz_coeffs", "s13", "s14", "s15"]
+        names = STAMP_SLOTS
         return dict(zip(names, list(out)))
 
     def reset_timing(self):

@@ -15,7 +15,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b((?:nr|netrep)_[A-Za-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b((?:nr|netrep)_[A-Za-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_expected_entry_points():

@@ -164,12 +164,63 @@ def test_c3_nulls_vs_cpp_oracle(c3):
     got = c3.eng.run(p0, p0 + 64, seed)
     exp, obs = c3.oracle(p0, p0 + 64, seed, True)
     gobs = c3.eng.observed()
+    # the metric's path: the Gram table, chosen from the shapes (the bench times this kernel)
+    assert c3.eng.gram_table()
     e1 = assert_stats_close(gobs, obs, what="C3 observed")
     e2 = assert_stats_close(got, exp, what="C3 nulls")
     record("C3 nulls (64 perms x 50 modules, S=500)", max(e1, e2), perms=64)
     k = np.diff(c3.node_off)
     record_pvalues("C3 (64 perms x 50 modules x 7 statistics)",
                    assert_pvalues_identical(got, gobs, exp, obs, k, c3.n, what="C3"))
+
+
+def _c3_disc_props(c3):
+    disc = {"degree": {}, "corr": {}, "contribution": {}}
+    o = ocv = 0
+    for m in c3.lay.modules:
+        k = c3.lay.members[m].size
+        disc["degree"][m] = c3.disc["degree"][o:o + k]
+        disc["contribution"][m] = c3.disc["contribution"][o:o + k]
+        disc["corr"][m] = c3.disc["corr"][ocv:ocv + k * (k - 1) // 2]
+        o += k
+        ocv += k * (k - 1) // 2
+    return disc
+
+
+def test_c3_two_contexts_table_bitwise(c3, monkeypatch):
+    """the metric's workload through netrep_PermutationProcedure
+    with NETREP_NUM_GPUS=2 and NETREP_SHARE_DEVICE=1 (two contexts on one GPU,
+    the dataset broadcast device to device, each context running its
+    contiguous chunk) is bitwise equal to one context and to the engine
+    layer's run of the same permutations; every context takes the Gram-table
+    path (chosen from the shapes). The engine-layer broadcast
+    (nr_broadcast_dataset) carries the table itself."""
+    seed, n_perm = 0x5EED, 48
+    ref = c3.eng.run(0, n_perm, seed)
+    assert c3.eng.gram_table()
+    names = c3.lay.names
+    ma = dict(zip(names, c3.lay.labels))
+    args = (_c3_disc_props(c3), RMatrix(c3.txs, None, names), RMatrix(c3.tc, names, names),
+            RMatrix(c3.tn, names, names), ma, c3.lay.modules, n_perm)
+    one = N.PermutationProcedure(*args, seed=seed)
+    np.testing.assert_array_equal(one["nulls"].view(np.uint64), ref.view(np.uint64))
+    monkeypatch.setenv("NETREP_NUM_GPUS", "2")
+    monkeypatch.setenv("NETREP_SHARE_DEVICE", "1")
+    two = N.PermutationProcedure(*args, seed=seed)
+    np.testing.assert_array_equal(two["nulls"].view(np.uint64), ref.view(np.uint64))
+    np.testing.assert_array_equal(two["observed"].view(np.uint64), one["observed"].view(np.uint64))
+    # engine layer: the broadcast copy of a context that holds the table
+    b = N.Engine(0)
+    try:
+        c3.eng.broadcast_dataset_to([b])
+        assert b.gram_table()
+        b.set_modules(len(c3.mods), c3.mods, c3.node_off, c3.idx, c3.idx, c3.disc["corr"], c3.disc["degree"],
+                      c3.disc["contribution"])
+        b.set_null_pool(np.arange(c3.n, dtype=np.int32))
+        got = b.run(0, n_perm, seed)
+        np.testing.assert_array_equal(got.view(np.uint64), ref.view(np.uint64))
+    finally:
+        b.close()
 
 
 def test_c4_network_only_full_size(c3):

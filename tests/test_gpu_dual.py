@@ -126,3 +126,22 @@ def test_netprops_beyond_lds():
             assert_stats_close(got[m][key], exp[m][key], what=f"{m}/{key}")
         assert_stats_close([got[m]["coherence"]], [exp[m]["coherence"]], what=f"{m}/coherence")
         assert_stats_close([got[m]["avgWeight"]], [exp[m]["avgWeight"]], what=f"{m}/avgWeight")
+
+
+@pytest.mark.parametrize("sizes,n_samples,seed,n_nodes", [([3000, 60], 3000, 93, 4500),
+                                                         ([2800, 33], 2600, 95, 4000)])
+def test_lanczos_dimension_beyond_lds_vectors(sizes, n_samples, seed, n_nodes):
+    """a 3,000-node module at S = 3,000 (primal) and a
+    2,800-node module at S = 2,600 (dual): Lanczos dimensions of 3,000 / 2,600,
+    beyond the ~2,540 LDS vectors, which round 3 rejected with
+    NR_ERR_UNSUPPORTED. They now run with every vector and the index set in the
+    slot's scratch (variant 6); svd_econ has no size limit
+    (src/netStats.cpp:217-250). Against the C++ LAPACK restatement on
+    identical shuffles."""
+    lay, mi, disc, txs, tc, tn = _case(sizes, n_samples, seed, n_nodes=n_nodes)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(4, 5, 17)
+    pis = N.prp_table(17, 4, 5, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what=f"observed (k {sizes[0]}, S {n_samples})")
+    assert_stats_close(nulls, exp, what=f"nulls (k {sizes[0]}, S {n_samples})")

@@ -1,0 +1,162 @@
+"""Residency across the reference-interface calls and the
+mesh broadcast of a resident dataset.
+
+modulePreservation loads each discovery dataset once and calls
+IntermediateProperties once per test dataset with it
+(R/modulePreservation.R:553-590); networkProperties calls NetProps per
+(discovery, test) pair (R/networkProperties.R:295-302). The library keeps
+those datasets in HBM while later calls name the same host arrays and counts
+every host->device byte (nr_h2d_bytes), so the tests can see what crossed
+PCIe. Results must be bitwise those of a fresh upload.
+
+nr_broadcast_dataset (scatter + all-gather of peer copies)
+must give every destination a bitwise copy: runs on the copies equal the
+source's run bit for bit, including sizes that do not split evenly.
+"""
+import numpy as np
+import pytest
+
+import netrep_amd as N
+from netrep_amd import synthetic as S
+from netrep_amd.api import RMatrix
+
+pytestmark = pytest.mark.gpu
+
+MB = 1 << 20
+
+
+def _dataset(n=2500, s=120, seed=11, sizes=(200, 150, 90, 40)):
+    lay = S.make_layout(n, list(sizes), seed)
+    x, c, nt = S.numpy_dataset(lay, s, seed + 1)
+    names = lay.names
+    return lay, names, dict(zip(names, lay.labels)), np.asfortranarray(x), np.asfortranarray(c), np.asfortranarray(nt)
+
+
+def _same(a, b):
+    for key in a:
+        if isinstance(a[key], dict):
+            assert a[key].keys() == b[key].keys()
+            for m in a[key]:
+                _same_arr(a[key][m], b[key][m])
+        else:
+            _same_arr(a[key], b[key])
+
+
+def _same_arr(x, y):
+    x, y = np.asarray(x, dtype=np.float64), np.asarray(y, dtype=np.float64)
+    np.testing.assert_array_equal(x.view(np.uint64), y.view(np.uint64))
+
+
+def test_discovery_dataset_uploaded_once_for_three_test_datasets():
+    """1 discovery x 3 test datasets: the discovery matrices cross PCIe once."""
+    N.ReleaseResident()
+    lay, names, ma, x, c, nt = _dataset()
+    dxs = N.Scale(RMatrix(x, None, names))
+    dc, dn = RMatrix(c, names, names), RMatrix(nt, names, names)
+    n, s = len(names), x.shape[0]
+    full = 2 * n * n * 8 + s * n * 8
+    rng = np.random.default_rng(3)
+    t_lists = [names, [nm for nm in names if rng.random() < 0.8], names[::2]]
+    outs, deltas = [], []
+    for t in t_lists:
+        before = N.h2d_bytes()
+        outs.append(N.IntermediateProperties(dxs, dc, dn, t, ma, lay.modules))
+        deltas.append(N.h2d_bytes() - before)
+    assert deltas[0] >= full, deltas
+    assert deltas[1] < MB and deltas[2] < MB, deltas
+    # a sampled element changed in place: the fingerprint no longer matches, re-upload
+    old = c[0, 0]
+    c[0, 0] = 0.5
+    before = N.h2d_bytes()
+    N.IntermediateProperties(dxs, dc, dn, t_lists[0], ma, lay.modules)
+    assert N.h2d_bytes() - before >= full
+    c[0, 0] = old
+    # bitwise the results of fresh uploads
+    for t, o in zip(t_lists, outs):
+        N.ReleaseResident()
+        _same(o, N.IntermediateProperties(dxs, dc, dn, t, ma, lay.modules))
+    N.ReleaseResident()
+
+
+def test_netprops_network_uploaded_once_and_kept():
+    """NetProps: the network crosses PCIe once (it is also the unused
+    correlation operand), the raw data once (scaled on the device), and a
+    second call on the same arrays uploads neither."""
+    N.ReleaseResident()
+    lay, names, ma, x, c, nt = _dataset(n=1800, s=90, seed=21, sizes=(160, 70, 33))
+    data, net = RMatrix(x, None, names), RMatrix(nt, names, names)
+    n, s = len(names), x.shape[0]
+    once = n * n * 8 + s * n * 8
+    b0 = N.h2d_bytes()
+    r1 = N.NetProps(data, net, ma, lay.modules)
+    d1 = N.h2d_bytes() - b0
+    assert once <= d1 < once + MB, (d1, once)
+    b1 = N.h2d_bytes()
+    r2 = N.NetProps(data, net, ma, lay.modules)
+    assert N.h2d_bytes() - b1 < MB
+    for m in r1:
+        for key in ("degree", "summary", "contribution"):
+            _same_arr(r1[m][key], r2[m][key])
+    # on-device scaling gives the same statistics as host-scaled data would
+    # within rounding (Scale on the device either way): compare with a fresh call
+    N.ReleaseResident()
+    r3 = N.NetProps(data, net, ma, lay.modules)
+    for m in r1:
+        _same_arr(r1[m]["summary"], r3[m]["summary"])
+        _same_arr([r1[m]["coherence"]], [r3[m]["coherence"]])
+    N.ReleaseResident()
+
+
+def test_pooled_contexts_give_identical_permutation_results():
+    """Contexts are reused across PermutationProcedure calls (no dataset
+    kept): repeated calls are bitwise equal, interleaved with other calls."""
+    N.ReleaseResident()
+    lay, names, ma, x, c, nt = _dataset(n=1500, s=80, seed=31, sizes=(120, 60, 31))
+    dxs = N.Scale(RMatrix(x, None, names))
+    disc = N.IntermediateProperties(dxs, RMatrix(c, names, names), RMatrix(nt, names, names), names, ma,
+                                    lay.modules)
+    tx, tc, tn = S.numpy_dataset(lay, 80, 32, preserve_all=False)
+    args = (disc, N.Scale(RMatrix(np.asfortranarray(tx), None, names)),
+            RMatrix(np.asfortranarray(tc), names, names), RMatrix(np.asfortranarray(tn), names, names),
+            ma, lay.modules, 40)
+    a = N.PermutationProcedure(*args, seed=5)
+    N.Scale(RMatrix(x, None, names))      # another call in between takes a pooled context too
+    b = N.PermutationProcedure(*args, seed=5)
+    _same_arr(a["nulls"], b["nulls"])
+    _same_arr(a["observed"], b["observed"])
+    N.ReleaseResident()
+
+
+@pytest.mark.parametrize("n,s", [(1001, 37), (640, 0)])
+def test_broadcast_dataset_three_contexts_bitwise(n, s):
+    """nr_broadcast_dataset to two contexts (pieces of uneven size): each copy
+    runs bitwise like the source, with and without data."""
+    from oracle import netrep_oracle as O
+    lay = S.make_layout(n, [120, 64, 30], 41)
+    x, c, nt = S.numpy_dataset(lay, max(s, 2), 42)
+    mi = O.ModuleIndex(lay.names, lay.labels, lay.names, lay.modules)
+    with_data = s > 0
+    disc = O.intermediate_properties(O.scale(x) if with_data else None, c, nt, mi.disc_idx(lay.names),
+                                     with_data=with_data)
+    mods = mi.mods_present
+    node_off = np.concatenate([[0], np.cumsum([mi.test_idx[m].size for m in mods])])
+    idx = np.concatenate([mi.test_idx[m] for m in mods])
+    engines = [N.Engine(0) for _ in range(3)]
+    try:
+        engines[0].set_dataset(c, nt, O.scale(x) if with_data else None)
+        engines[0].broadcast_dataset_to(engines[1:])
+        outs = []
+        for e in engines:
+            assert e.shape() == (n, s if with_data else 0)
+            e.set_modules(len(mi.modules), [mi.modules.index(m) for m in mods], node_off, idx,
+                          np.concatenate([mi.null_pos[m] for m in mods]),
+                          np.concatenate([disc["corr"][m] for m in mods]),
+                          np.concatenate([disc["degree"][m] for m in mods]),
+                          np.concatenate([disc["contribution"][m] for m in mods]) if with_data else None)
+            e.set_null_pool(mi.null_idx)
+            outs.append(e.run(3, 19, 8))
+        for o in outs[1:]:
+            _same_arr(outs[0], o)
+    finally:
+        for e in engines:
+            e.close()

@@ -37,6 +37,8 @@ def test_small_class_primal_only_vs_cpp_oracle():
     lay, mi, disc, txs, tc, tn = _case([112, 96, 64, 33, 16], 300, 73, n_nodes=1200)
     eng = _engine_from(mi, disc, txs, tc, tn)
     nulls = eng.run(0, 16, 5)
+    # small-class launch: no fused packed segment, so no Gram table
+    assert not eng.gram_table()
     pis = N.prp_table(5, 0, 16, mi.null_idx.size)
     exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
     assert_stats_close(eng.observed(), obs, what="observed (small class, primal)")
