@@ -54,7 +54,8 @@ struct nr_ctx {
 
   // resident dataset
   double2* d_pairs = nullptr;
-  int32_t pairs_es = 1;          // d_pairs element stride in double2: 2 = the Gram table layout
+  int32_t pairs_es = 1;          // d_pairs element stride in double2: 2 = the Gram table layout,
+                                 // 0 = the packed lower triangle (symmetric matrices; pack rule below)
   double* d_colsum = nullptr;    // [n_nodes] column sums of the data (Gram table)
   int64_t table_checked = -1;    // modules_serial the Gram-table decision was made for
   double table_ms = 0.0;         // wall time of the last Gram-table build
@@ -221,6 +222,37 @@ int fill_na(nr_ctx* ctx, double* d, int64_t n, hipStream_t st = nullptr) {
 }
 
 int n_stat_of(const nr_ctx* ctx) { return ctx->d_data ? NR_NSTAT_DATA : NR_NSTAT_NODATA; }
+
+// Bytes of the resident {corr, net} array in its layout (pairs_es).
+size_t pair_bytes_of(const nr_ctx* ctx) {
+  const size_t n = (size_t)ctx->n_nodes;
+  return ctx->pairs_es == 0 ? n * (n + 1) / 2 * sizeof(double2) : n * n * sizeof(double2) * (size_t)ctx->pairs_es;
+}
+
+// Symmetric matrices whose packed lower triangle fits the 256 MiB Infinity
+// Cache (n <= 5,792: C2's 5,000 genes) are kept as that triangle: every
+// CorrVector / WeightedDegree gather then hits the on-die cache instead of
+// a 2x larger full matrix that does not fit it. The rule depends on the
+// shape and the (exact) symmetry only; results are bitwise the same.
+#ifndef NR_PACK_PAIRS
+#define NR_PACK_PAIRS 1  // tuning: 0 never, 1 when the triangle fits the Infinity Cache, 2 every symmetric dataset
+#endif
+int maybe_pack_pairs(nr_ctx* ctx, int64_t n) {
+  if (!ctx->symmetric || ctx->pairs_es != 1 || NR_PACK_PAIRS == 0 || n > 65535) return NR_OK;
+  if (NR_PACK_PAIRS == 1 && 8 * n * n > ((int64_t)256 << 20)) return NR_OK;
+  double2* tri = nullptr;
+  NR_HIP(ctx, hipMalloc((void**)&tri, (size_t)(n * (n + 1) / 2) * sizeof(double2)));
+  hipError_t e = nr::launch_pack_pairs(ctx->d_pairs, tri, n, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    (void)hipFree(tri);
+    return hip_fail(ctx, e, "pack pairs");
+  }
+  dfree(ctx->d_pairs);
+  ctx->d_pairs = tri;
+  ctx->pairs_es = 0;
+  return NR_OK;
+}
 
 // No dataset: buffers freed, shape zero. Modules validated against an earlier
 // dataset (their node indices) stop being usable: check_ready demands a new
@@ -466,6 +498,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
   // every segment's scratch (slots x stride) is one allocation, carved in turn
   int64_t total = 0;
   bool fuse[2] = {false, false};
+  int fuse_kind[2] = {0, 0};  // ProfileParams::fused
   for (int i = 0; i < ns; ++i) {
     const int rc = plan_profile(ctx, (int64_t)seg[i].count * n_perm, k_sorted[seg[i].first], (int)pp.n_samples,
                                 &seg[i].plan);
@@ -474,16 +507,26 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     // its network statistics and Gram from the table's gathers, on the table
     // kernel's own workgroup shape
     const int k_max = k_sorted[seg[i].first];
-    fuse[i] = table_np && seg[i].plan.variant == 2 && k_max <= nr::kPackedLayoutK && k_max <= pp.n_samples &&
-              nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
+    const bool fuse_table = table_np && table_np->es == 2 && seg[i].plan.variant == 2 &&
+                            k_max <= nr::kPackedLayoutK && k_max <= pp.n_samples &&
+                            nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
+    // the small class computes its items' network statistics from the
+    // {corr, net} pairs itself (symmetric matrices; launch_batch passes the
+    // pairs only then)
+    const bool fuse_small = table_np && table_np->es == 1 && seg[i].plan.variant == 5 && i == ns - 1;
+    fuse_kind[i] = fuse_table ? 1 : fuse_small ? 2 : 0;
+    fuse[i] = fuse_kind[i] != 0;
 #ifndef NR_TABLE_G32
 #define NR_TABLE_G32 1
 #endif
-    if (fuse[i] && !NR_TABLE_G32) seg[i].plan.g32_off = 0;  // tuning: no fp32 copy, no relaxed steps
-    if (fuse[i] && nr::kTableWaves != nr::kProfileWaves) {
+    if (fuse_kind[i] == 1 && !NR_TABLE_G32) seg[i].plan.g32_off = 0;  // tuning: no fp32 copy, no relaxed steps
+#ifndef NR_TABLE_RESIDENT
+#define NR_TABLE_RESIDENT 0  // tuning: 1 = the one-per-CU 8-wave kernel (measured 1.8x slower, profiles/r04/)
+#endif
+    if (fuse_kind[i] == 1 && (NR_TABLE_RESIDENT || nr::kTableWaves != nr::kProfileWaves)) {
       int dev_cu = 256;
       (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-      seg[i].plan.per_cu = nr::profile_table_per_cu();
+      seg[i].plan.per_cu = NR_TABLE_RESIDENT ? 1 : nr::profile_table_per_cu();
       seg[i].plan.slots = (int)std::max<int64_t>(
           1, std::min<int64_t>((int64_t)seg[i].count * n_perm, (int64_t)dev_cu * seg[i].plan.per_cu));
     }
@@ -514,7 +557,15 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
                                     : profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm,
                                                          (int)pp.n_samples);
     pp.g32_off = plan.g32_off;
-    pp.fused = fuse[i];
+    pp.fused = fuse_kind[i];
+    pp.lds_gram_n = 0;
+    if (pp.fused == 1 && NR_TABLE_RESIDENT) {
+      // the CU-resident kernel: one workgroup per CU, the Gram's leading units
+      // in LDS; permutation-major order keeps a size mix in flight, so the
+      // rest of the Grams (the slots' scratch) stays in the XCDs' L2
+      pp.lds_gram_n = nr::profile_resident_gram_doubles();
+      pp.order_tail = (int)std::min<int64_t>(n_perm - 1, (plan.slots + seg[i].count - 1) / seg[i].count);
+    }
     if (pp.fused) {
       pp.net = *table_np;
       pp.net.mod_order = pp.mod_order;
@@ -647,6 +698,9 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   // phase fused into the profile items without the table at +0.7%, within
   // run-to-run noise, and on a concurrent stream at -11%.)
   const bool table = data && ctx->pairs_es == 2;
+  // the small class's launch computes its own items' network statistics
+  // (fused == 2) for symmetric matrices
+  const bool small_fuse = data && !table && ctx->symmetric && nr::small_fuse_enabled();
   auto nets = [&](int n_mod) -> int {
     if (n_mod <= 0) return NR_OK;
     std::vector<int32_t> ks(ctx->order_k_h.begin(), ctx->order_k_h.begin() + n_mod);
@@ -655,7 +709,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     if (ln.timed) timer_end(ctx, 0, (int64_t)n_mod * n_perm, ln.st);
     return NR_OK;
   };
-  if (!table && (rc = nets(ctx->n_present))) return rc;
+  if (!table && !small_fuse && (rc = nets(ctx->n_present))) return rc;
 
   if (data) {
     nr::ProfileParams pp{};
@@ -678,11 +732,11 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.stamps = ln.timed ? ctx->d_stamps : nullptr;
     int fused_from = ctx->n_present;
     if (ln.timed) timer_begin(ctx, 1, ln.st);
-    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ln, table ? &np : nullptr,
-                         &fused_from);
+    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ln,
+                         table || small_fuse ? &np : nullptr, &fused_from);
     if (rc) return rc;
     if (ln.timed) timer_end(ctx, 1, n_items, ln.st);
-    if (table && (rc = nets(fused_from))) return rc;
+    if ((table || small_fuse) && (rc = nets(fused_from))) return rc;
   }
   if (ln.timed) timer_collect(ctx);
   return NR_OK;
@@ -746,8 +800,11 @@ int maybe_build_table(nr_ctx* ctx) {
     dfree(tab);
     dfree(cs);
   };
+#ifndef NR_TABLE_ALLOC
+#define NR_TABLE_ALLOC 0  // tuning: the table's allocation flags (hipExtMallocWithFlags; 3 = uncached)
+#endif
   if (hipMalloc((void**)&gram, nn * sizeof(double)) != hipSuccess ||
-      hipMalloc((void**)&tab, 2 * nn * sizeof(double2)) != hipSuccess ||
+      hipExtMallocWithFlags((void**)&tab, 2 * nn * sizeof(double2), NR_TABLE_ALLOC) != hipSuccess ||
       hipMalloc((void**)&cs, (size_t)n * sizeof(double)) != hipSuccess) {
     drop();
     (void)hipGetLastError();
@@ -758,7 +815,8 @@ int maybe_build_table(nr_ctx* ctx) {
                     "from the shapes, DESIGN.md section 5.2)");
   }
   hipError_t e = nr::launch_gram_full(ctx->d_data, S, n, gram, cs, ctx->stream);
-  if (e == hipSuccess) e = nr::launch_widen_pairs(ctx->d_pairs, gram, tab, n, ctx->symmetric, ctx->stream);
+  if (e == hipSuccess)
+    e = nr::launch_widen_pairs(ctx->d_pairs, gram, tab, n, ctx->symmetric, ctx->pairs_es == 0, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     drop();
@@ -1194,6 +1252,7 @@ int set_dataset_impl(nr_ctx* ctx, const double* corr, const double* net, const d
   ctx->symmetric = (asym & 1) ? 0 : 1;
   ctx->corr_finite = (asym & 2) ? 0 : 1;
   ctx->net_finite = (asym & 4) ? 0 : 1;
+  if (int rc = maybe_pack_pairs(ctx, n_nodes)) return rc;
   ctx->n_nodes = n_nodes;
   ctx->n_samples = data ? n_samples : 0;
   return NR_OK;
@@ -1307,6 +1366,7 @@ int set_dataset_files_impl(nr_ctx* ctx, const char* corr_path, const char* net_p
   ctx->symmetric = (asym & 1) ? 0 : 1;
   ctx->corr_finite = (asym & 2) ? 0 : 1;
   ctx->net_finite = (asym & 4) ? 0 : 1;
+  if ((rc = maybe_pack_pairs(ctx, n_nodes))) return rc;
   // committed only once everything above has succeeded
   ctx->node_names = names;
   ctx->n_nodes = n_nodes;
@@ -1368,7 +1428,7 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
   NR_HIP(dst, hipSetDevice(dst->device));
   NR_HIP(dst, hipStreamSynchronize(dst->stream));
   reset_dataset(dst);  // on a failure below dst is left with no dataset
-  const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2) * (size_t)src->pairs_es;
+  const size_t pair_bytes = pair_bytes_of(src);
   NR_HIP(dst, hipMalloc((void**)&dst->d_pairs, pair_bytes));
   if (src->d_colsum) NR_HIP(dst, hipMalloc((void**)&dst->d_colsum, (size_t)src->n_nodes * sizeof(double)));
   const size_t data_bytes = (size_t)(src->n_samples * (src->n_nodes + 2)) * sizeof(double);  // + virtual columns
@@ -1419,7 +1479,7 @@ int nr_broadcast_dataset(nr_ctx* const* ctxs, int n) {
     size_t bytes;
   };
   std::vector<Buf> bufs;
-  const size_t pair_bytes = (size_t)(src->n_nodes * src->n_nodes) * sizeof(double2) * (size_t)src->pairs_es;
+  const size_t pair_bytes = pair_bytes_of(src);
   const size_t data_bytes = (size_t)(src->n_samples * (src->n_nodes + 2)) * sizeof(double);  // + virtual columns
   const size_t cs_bytes = (size_t)src->n_nodes * sizeof(double);
   bufs.push_back({reinterpret_cast<const char*>(src->d_pairs), std::vector<char*>(n, nullptr), pair_bytes});

@@ -37,8 +37,9 @@ struct IndexSource {
 
 struct NetParams {
   const double2* pairs;        // interleaved {corr, net}, column-major n x n (es = 1), or the
-                               // Gram table: {corr, net}, {gram, net^T} per (i, j) (es = 2)
-  int32_t es;                  // element stride of pairs in double2 units (1 or 2)
+                               // Gram table: {corr, net}, {gram, net^T} per (i, j) (es = 2), or the
+                               // packed lower triangle of symmetric matrices (es = 0)
+  int32_t es;                  // element stride of pairs in double2 units (1 or 2; 0: packed)
   const double* colsum;        // [n_nodes] column sums of the data (Gram table only)
   int64_t n_nodes;
   int symmetric;               // both matrices exactly symmetric
@@ -106,8 +107,10 @@ struct ProfileParams {
   // Gram table (packed kernel only): the network statistics of each item are
   // computed in the profile workgroup from one gather per pair of the table,
   // which also fills the item's packed Gram (no matrix-core Gram for k <= S)
-  int32_t fused;
+  int32_t fused;                // 1: Gram-table items (network statistics + Gram from the table);
+                               // 2: the small class with its network statistics in the same workgroup
   NetParams net;
+  int64_t lds_gram_n;          // resident kernel: LDS doubles for the Gram's leading units (0: not resident)
 };
 
 size_t net_kernel_lds(int k_max);
@@ -129,6 +132,16 @@ bool fused_net_fits(int kvec, int mmax, int nw);
 constexpr int kTableWaves = NR_TABLE_WAVES;
 size_t profile_table_lds();
 int profile_table_per_cu();
+// LDS doubles the table kernel keeps for its item's Gram prefix (NR_TABLE_LDS)
+int64_t profile_table_gram_lds_doubles();
+// The CU-resident Gram-table kernel (one workgroup of kResWaves waves per
+// CU): its LDS carve-out bytes, and the LDS doubles left for the Gram.
+#ifndef NR_RES_WAVES
+#define NR_RES_WAVES 8
+#endif
+constexpr int kResWaves = NR_RES_WAVES;
+size_t profile_resident_carve();
+int64_t profile_resident_gram_doubles();
 // The Gram table of a dataset with data: gram[i + j n] = x_i . x_j over the
 // n_samples rows of X (n_samples x (n + 2), the virtual columns behind), and
 // colsum[j] = sum of column j.
@@ -136,10 +149,16 @@ hipError_t launch_gram_full(const double* X, int64_t S, int64_t n, double* gram,
 // {corr, net} pairs (es = 1) + gram -> the table layout (es = 2):
 // out[2e] = in[e], out[2e + 1] = {gram[e], net(j, i)} for e = i + j n.
 hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* out, int64_t n, int symmetric,
-                              hipStream_t st);
+                              int packed, hipStream_t st);
+// full n x n {corr, net} pairs -> the packed lower triangle (es = 0; symmetric matrices only)
+hipError_t launch_pack_pairs(const double2* in, double2* out, int64_t n, hipStream_t st);
 // the small class (variant 5): its LDS bytes per workgroup and workgroups per CU
 size_t profile_small_lds();
 int profile_small_per_cu();
+// whether the small class computes its items' network statistics itself (NR_SMALL_FUSE),
+// and its LDS bytes per workgroup then (the network arrays of k_max-node modules)
+bool small_fuse_enabled();
+size_t small_fused_lds(int k_max);
 // variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch,
 // 5 the small class, 6 full Gram with the partials and every vector in scratch
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
