@@ -81,12 +81,16 @@ def test_contingency_partial_overlap_and_test_modules():
 
 def test_bench_traffic_lookup_matches_committed_pmc():
     """bench.py reports `roofline.traffic` only from a PMC pass of the same
-    config, batch and kernel (profiles/pmc_traffic.json)."""
+    config, batch and kernel (profiles/pmc_traffic.json), as a [raw, x2] range
+    with the pass's kernel time next to this run's (traffic_time_ratio)."""
     import bench
-    t = bench.measured_traffic("C3", 256, "module_profile_kernel")
-    assert t is not None and t > 0
-    assert bench.measured_traffic("C3", 512, "module_profile_kernel") is None
-    assert bench.measured_traffic("C2", 256, "module_profile_kernel") is None
+    t = bench.traffic_fields("C3", 256, "module_profile_kernel", 17.9)
+    assert t["traffic"] is not None and t["traffic"] > 0
+    raw, x2 = t["traffic_range"]
+    assert 0 < raw <= x2 == t["traffic"]
+    assert abs(t["traffic_time_ratio"] - 1.0) < 0.01     # the r02 pass: 17.915 ms
+    assert bench.traffic_fields("C3", 512, "module_profile_kernel", 1.0)["traffic"] is None
+    assert bench.traffic_fields("C2", 256, "module_profile_kernel", 1.0)["traffic"] is None
 
 
 def test_vars_present_aligned_by_label_from_contingency():
