@@ -80,6 +80,10 @@ def traffic_fields(config, batch, kernel, avg_ms, table=False):
            "traffic_source": r.get("source"), "traffic_pass_avg_ms": r["avg_ns_rocprof"] / 1e6}
     if avg_ms > 0:
         out["traffic_time_ratio"] = round(r["avg_ns_rocprof"] / 1e6 / avg_ms, 4)
+        # the bytes the kernel actually moves past L2 per second, against HBM peak
+        # (Infinity-Cache hits included, so this can exceed what HBM alone delivers)
+        out["traffic_GBps"] = round(float(r["hbm_bytes_per_launch"]) / (avg_ms * 1e-3) / 1e9, 1)
+        out["traffic_frac_of_hbm_peak"] = round(out["traffic_GBps"] / HBM_PEAK_GBS, 4)
     return out
 
 

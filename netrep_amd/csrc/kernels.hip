@@ -53,6 +53,12 @@
 #define NR_G64_PINGPONG 0
 #endif
 
+// the large modules' Gram in 128 x 128 workgroup tiles staged through LDS
+// (gram_mfma128); 0: the per-wave 64 x 64 tiles of round 3
+#ifndef NR_BIG_G128
+#define NR_BIG_G128 1
+#endif
+
 // Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta.
 #ifndef NR_LZ_TOL
 #define NR_LZ_TOL 5e-15
@@ -1141,6 +1147,150 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
   }
 }
 
+// 128 x 128 workgroup tiles of the large modules' Gram (primal [X 1]^T[X 1]
+// or the dual H of k > S), four waves as 2 x 2 sub-tiles of 64 x 64 (each
+// the 4 x 4 MFMA tiles of gram_mfma64, same K order within a 16-step and
+// the same epilogue). Each 16-deep K step of the tile's two operand slices
+// (128 columns x 16 each) is loaded from global once per workgroup into LDS
+// and read by the waves that share it: half the operand traffic of
+// gram_mfma64's independent per-wave tiles, which made the large items'
+// Gram operand-bound at ~55% of the MFMA peak (C5).
+// The staging overlays the Lanczos vectors and matvec partials (idle until
+// the Lanczos phase; the caller zeroes the partials again), double-buffered
+// when they hold two stages (one barrier per K step), else single-buffered.
+// Row stride 132 doubles: the two K rows a ds_read_b64 lane group reads (4
+// rows apart) fall on disjoint bank halves.
+constexpr int kG128Ld = 132;
+constexpr int kG128Stage = 2 * 16 * kG128Ld;  // doubles of one stage (A and B slices)
+
+template <int NW, bool DUAL>
+__device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t* idx, int k, int64_t ones_off,
+                             double* __restrict__ G, float* __restrict__ G32, double& g1sum, int& bad,
+                             double* stage, int n_stages) {
+  static_assert(NW == 4, "2 x 2 waves per 128 x 128 tile");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wa = wave >> 1, wb = wave & 1;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int kc = DUAL ? S + 1 : k + 1;
+  const int T4 = (kc + 63) / 64;
+  const int T8 = (kc + 127) / 128;
+  const int nsup = T8 * (T8 + 1) / 2;
+  const int kdim = DUAL ? k : S;  // contraction length
+  const int nsteps = (kdim + 15) / 16;
+  // one thread's share of a K step: 8 consecutive elements of one operand
+  // column, for the row slice (A, rows of I8) and the column slice (B, J8)
+  const int gr = DUAL ? (tid & 15) * 8 : tid >> 1;  // tile row (first of 8 for DUAL)
+  const int gk = DUAL ? tid >> 4 : (tid & 1) * 8;   // K row (first of 8 for primal)
+  for (int t = 0; t < nsup; ++t) {
+    int I8 = 0, rem = t;
+    while (rem >= T8 - I8) { rem -= T8 - I8; ++I8; }
+    const int J8 = I8 + rem;
+    const int I4 = 2 * I8 + wa, J4 = 2 * J8 + wb;
+    const bool active = I4 <= J4 && J4 < T4;  // uniform over the wave
+    const bool diag = I4 == J4;
+    nr_f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+    double ra[8], rb[8];
+    auto gload = [&](int step) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double* dst = h == 0 ? ra : rb;
+        const int base = 128 * (h == 0 ? I8 : J8);
+        if (DUAL) {
+          const int c = 16 * step + gk;  // node
+          const bool valid = c < k;
+          const double* colp = X + (int64_t)idx[valid ? c : k - 1] * S;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int sm = base + gr + e;  // sample
+            const double x = sm < S ? colp[sm] : (sm == S ? 1.0 : 0.0);
+            dst[e] = valid ? x : 0.0;
+          }
+        } else {
+          const int c = base + gr;  // node (k: the ones column, beyond: the zero column)
+          const double* colp = X + (c < k ? (int64_t)idx[c] * S : (c == k ? ones_off : ones_off + S));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int sm = 16 * step + gk + e;
+            dst[e] = sm < S ? colp[sm] : 0.0;
+          }
+        }
+      }
+    };
+    auto sstore = [&](double* buf) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double* v = h == 0 ? ra : rb;
+        double* sl = buf + h * 16 * kG128Ld;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (DUAL) sl[gk * kG128Ld + gr + e] = v[e];
+          else sl[(gk + e) * kG128Ld + gr] = v[e];
+        }
+      }
+    };
+    auto compute = [&](const double* buf) {
+      const double* sa = buf;
+      const double* sb = buf + 16 * kG128Ld;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kr = 4 * kk + q;  // gram_mfma64's K order within the step
+        double va[4], vb[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) va[a] = sa[kr * kG128Ld + 64 * wa + 16 * a + i16];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) vb[b] = sb[kr * kG128Ld + 64 * wb + 16 * b + i16];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            if (!diag || b >= a) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[a], vb[b], acc[a][b], 0, 0, 0);
+      }
+    };
+    if (nsteps > 0) {
+      gload(0);
+      sstore(stage);
+    }
+    __syncthreads();
+    for (int i = 0; i < nsteps; ++i) {
+      const double* cur = n_stages == 2 ? stage + (i & 1) * kG128Stage : stage;
+      const bool more = i + 1 < nsteps;
+      if (more) gload(i + 1);  // in flight during this step's MFMAs
+      if (active) compute(cur);
+      if (n_stages == 1) __syncthreads();  // every wave has read the single stage
+      if (more) sstore(n_stages == 2 ? stage + ((i + 1) & 1) * kG128Stage : stage);
+      __syncthreads();
+    }
+    if (active) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (diag && b < a) continue;
+          pk_store_tile16(G, G32, kc, 4 * I4 + a, 4 * J4 + b, acc[a][b], lane);
+          const double wgt = (diag && a == b) ? 1.0 : 2.0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // D[row = (lane>>4) + 4r][col = lane & 15] (f64 MFMA C/D map)
+            const int gi = (4 * I4 + a) * 16 + kk + 4 * r;
+            const int gj = (4 * J4 + b) * 16 + i16;
+            const double val = acc[a][b][r];
+            if (DUAL) {
+              if (gj == S && gi < S) g1sum += val * val;  // |X 1|^2 from the row sums
+              if (gi == gj && gi < S) bad |= (int)!isfinite(val);
+            } else {
+              if (gi < k && gj < k) g1sum += wgt * val;
+              if (gi == gj && gi < k) bad |= (int)!isfinite(val);
+            }
+          }
+        }
+    }
+  }
+}
+
 // Dual Gram for modules with more nodes than samples (k > S): H = [X' 1]' [X' 1]
 // over the k module nodes, i.e. X X' (S x S) bordered by the row sums X 1 and
 // k. Its top eigenvector is the summary profile u itself (the left singular
@@ -1870,10 +2020,21 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     }
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     if (G64) {
-      if (dual)
+      // the 128 x 128 workgroup tiles when the idle Lanczos vectors and
+      // partials hold a stage of operand slices (NR_BIG_G128)
+      const int64_t cap = 6 * (int64_t)kmax + n_part;
+      const int stages = !NR_BIG_G128 ? 0 : cap >= 2 * kG128Stage ? 2 : (cap >= kG128Stage ? 1 : 0);
+      if (NW == 4 && stages > 0) {
+        if (dual)
+          gram_mfma128<NW == 4 ? 4 : 4, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad, L.q, stages);
+        else
+          gram_mfma128<NW == 4 ? 4 : 4, false>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad, L.q, stages);
+        for (int64_t i = tid; i < n_part; i += BS) part[i] = 0.0;  // the staging overlapped them
+      } else if (dual) {
         gram_mfma64<NW, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
-      else
+      } else {
         gram_mfma64<NW, false>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad);
+      }
     } else if (!TABLE) {
       if (dual)
         gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
