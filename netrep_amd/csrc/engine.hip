@@ -109,6 +109,10 @@ struct nr_ctx {
   double* h_stage2 = nullptr;
   size_t stage2_cap = 0;
   hipEvent_t ev_copy[2] = {nullptr, nullptr};
+  // NR_NET_SIDE: the network launch on a stream of its own beside the
+  // profile launches (per lane: main, observed), forked/joined by events
+  hipStream_t net_stream[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
 
   // The observed statistics' own lane (nr_observed_async): stream, scratch and
   // work queue, so that they run beside the first permutation batch instead
@@ -229,19 +233,26 @@ size_t pair_bytes_of(const nr_ctx* ctx) {
   return ctx->pairs_es == 0 ? n * (n + 1) / 2 * sizeof(double2) : n * n * sizeof(double2) * (size_t)ctx->pairs_es;
 }
 
-// Symmetric matrices whose packed lower triangle fits the 256 MiB Infinity
-// Cache (n <= 5,792: C2's 5,000 genes) are kept as that triangle: every
-// CorrVector / WeightedDegree gather then hits the on-die cache instead of
-// a 2x larger full matrix that does not fit it. The rule depends on the
-// shape and the (exact) symmetry only; results are bitwise the same.
+// Symmetric matrices of more than 8,192 nodes (a full {corr, net} array
+// beyond 1 GiB) are kept as their packed lower triangle: the network gathers
+// then spread over half the footprint (fewer DRAM pages and translations per
+// gather). Measured (profiles/r04/ab4): C4 (20,000 nodes) 60.3k -> 64.8k
+// perms/s packed; C2 (5,000 nodes, its 400 MB full array mostly in the
+// Infinity Cache) 75.0k full vs 72.1k packed (the triangle's index
+// arithmetic). The rule depends on the shape and the (exact) symmetry only;
+// results are bitwise the same. No memory for the triangle: the full array
+// stays.
 #ifndef NR_PACK_PAIRS
-#define NR_PACK_PAIRS 1  // tuning: 0 never, 1 when the triangle fits the Infinity Cache, 2 every symmetric dataset
+#define NR_PACK_PAIRS 1  // tuning: 0 never, 1 beyond 8,192 nodes, 2 every symmetric dataset
 #endif
 int maybe_pack_pairs(nr_ctx* ctx, int64_t n) {
   if (!ctx->symmetric || ctx->pairs_es != 1 || NR_PACK_PAIRS == 0 || n > 65535) return NR_OK;
-  if (NR_PACK_PAIRS == 1 && 8 * n * n > ((int64_t)256 << 20)) return NR_OK;
+  if (NR_PACK_PAIRS == 1 && n <= 8192) return NR_OK;
   double2* tri = nullptr;
-  NR_HIP(ctx, hipMalloc((void**)&tri, (size_t)(n * (n + 1) / 2) * sizeof(double2)));
+  if (hipMalloc((void**)&tri, (size_t)(n * (n + 1) / 2) * sizeof(double2)) != hipSuccess) {
+    (void)hipGetLastError();
+    return NR_OK;
+  }
   hipError_t e = nr::launch_pack_pairs(ctx->d_pairs, tri, n, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
@@ -462,16 +473,17 @@ struct Lane {
   size_t* net_cap;
   int* counters;  // [0] queue head, [1..4] Lanczos diagnostics
   bool timed;     // kernel timers (nr_set_timing) follow the main lane only
+  int id;         // 0 = main, 1 = observed (the lane's side stream)
 };
 
 Lane main_lane(nr_ctx* ctx) {
   return {ctx->stream, &ctx->d_scratch, &ctx->scratch_cap, &ctx->d_net_scratch, &ctx->net_scratch_cap,
-          ctx->d_counters, true};
+          ctx->d_counters, true, 0};
 }
 
 Lane obs_lane(nr_ctx* ctx) {
   return {ctx->obs_stream, &ctx->obs_scratch, &ctx->obs_scratch_cap, &ctx->obs_net_scratch, &ctx->obs_net_cap,
-          ctx->obs_counters, false};
+          ctx->obs_counters, false, 1};
 }
 
 // Summary-profile launches over the module order sorted by size (descending,
@@ -655,6 +667,10 @@ int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std
   return NR_OK;
 }
 
+#ifndef NR_NET_SIDE
+#define NR_NET_SIDE 0  // tuning: 1 = the unfused network launch on a side stream, concurrent with the profiles
+#endif
+
 // Launch the statistics kernels for n_perm permutations (or the observed /
 // direct sets when src.mode == NR_IDX_DIRECT, n_perm == 1) into d_out.
 int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double* d_out, const Lane& ln) {
@@ -709,7 +725,29 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     if (ln.timed) timer_end(ctx, 0, (int64_t)n_mod * n_perm, ln.st);
     return NR_OK;
   };
-  if (!table && !small_fuse && (rc = nets(ctx->n_present))) return rc;
+  // NR_NET_SIDE: without fusion the network launch runs on the lane's side
+  // stream concurrently with the profile launches (both only write their own
+  // statistic rows of d_out, after fill_na); the lane's stream joins it.
+  const bool side = NR_NET_SIDE && data && !table && !small_fuse;
+  if (side) {
+    const int id = ln.id;
+    if (!ctx->net_stream[id]) {
+      NR_HIP(ctx, hipStreamCreateWithFlags(&ctx->net_stream[id], hipStreamNonBlocking));
+      NR_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork[id], hipEventDisableTiming));
+      NR_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join[id], hipEventDisableTiming));
+    }
+    NR_HIP(ctx, hipEventRecord(ctx->ev_fork[id], ln.st));
+    NR_HIP(ctx, hipStreamWaitEvent(ctx->net_stream[id], ctx->ev_fork[id], 0));
+    Lane sl = ln;
+    sl.st = ctx->net_stream[id];
+    std::vector<int32_t> ks(ctx->order_k_h.begin(), ctx->order_k_h.begin() + ctx->n_present);
+    if (sl.timed) timer_begin(ctx, 0, sl.st);
+    if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ks, n_perm, sl))) return rc;
+    if (sl.timed) timer_end(ctx, 0, (int64_t)ctx->n_present * n_perm, sl.st);
+    NR_HIP(ctx, hipEventRecord(ctx->ev_join[id], sl.st));
+  } else if (!table && !small_fuse && (rc = nets(ctx->n_present))) {
+    return rc;
+  }
 
   if (data) {
     nr::ProfileParams pp{};
@@ -738,6 +776,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     if (ln.timed) timer_end(ctx, 1, n_items, ln.st);
     if ((table || small_fuse) && (rc = nets(fused_from))) return rc;
   }
+  if (side) NR_HIP(ctx, hipStreamWaitEvent(ln.st, ctx->ev_join[ln.id], 0));
   if (ln.timed) timer_collect(ctx);
   return NR_OK;
 }
@@ -1087,6 +1126,11 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   for (auto& ev : ctx->ev_copy)
     if (ev) (void)hipEventDestroy(ev);
   if (ctx->obs_stream) (void)hipStreamDestroy(ctx->obs_stream);
+  for (int i = 0; i < 2; ++i) {
+    if (ctx->net_stream[i]) (void)hipStreamDestroy(ctx->net_stream[i]);
+    if (ctx->ev_fork[i]) (void)hipEventDestroy(ctx->ev_fork[i]);
+    if (ctx->ev_join[i]) (void)hipEventDestroy(ctx->ev_join[i]);
+  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -1160,6 +1160,9 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
 // when they hold two stages (one barrier per K step), else single-buffered.
 // Row stride 132 doubles: the two K rows a ds_read_b64 lane group reads (4
 // rows apart) fall on disjoint bank halves.
+#ifndef NR_G128_PF
+#define NR_G128_PF 2  // global-load distance in K steps (1: the next step only)
+#endif
 constexpr int kG128Ld = 132;
 constexpr int kG128Stage = 2 * 16 * kG128Ld;  // doubles of one stage (A and B slices)
 
@@ -1193,11 +1196,11 @@ __device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
-    double ra[8], rb[8];
-    auto gload = [&](int step) {
+    double ra[2][8], rb[2][8];  // register sets of two K steps (NR_G128_PF == 2 uses both)
+    auto gload = [&](int step, int set) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        double* dst = h == 0 ? ra : rb;
+        double* dst = h == 0 ? ra[set] : rb[set];
         const int base = 128 * (h == 0 ? I8 : J8);
         if (DUAL) {
           const int c = 16 * step + gk;  // node
@@ -1220,10 +1223,10 @@ __device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t
         }
       }
     };
-    auto sstore = [&](double* buf) {
+    auto sstore = [&](double* buf, int set) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const double* v = h == 0 ? ra : rb;
+        const double* v = h == 0 ? ra[set] : rb[set];
         double* sl = buf + h * 16 * kG128Ld;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -1250,19 +1253,40 @@ __device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t
             if (!diag || b >= a) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[a], vb[b], acc[a][b], 0, 0, 0);
       }
     };
-    if (nsteps > 0) {
-      gload(0);
-      sstore(stage);
-    }
-    __syncthreads();
-    for (int i = 0; i < nsteps; ++i) {
-      const double* cur = n_stages == 2 ? stage + (i & 1) * kG128Stage : stage;
-      const bool more = i + 1 < nsteps;
-      if (more) gload(i + 1);  // in flight during this step's MFMAs
-      if (active) compute(cur);
-      if (n_stages == 1) __syncthreads();  // every wave has read the single stage
-      if (more) sstore(n_stages == 2 ? stage + ((i + 1) & 1) * kG128Stage : stage);
+    if (NR_G128_PF == 2 && n_stages == 2) {
+      // global loads two K steps ahead (register sets alternate), LDS stages one
+      // step ahead: a step's operands have two steps of MFMAs (~8,000 cycles)
+      // to arrive instead of one
+      if (nsteps > 0) gload(0, 0);
+      if (nsteps > 1) gload(1, 1);
+      if (nsteps > 0) sstore(stage, 0);
       __syncthreads();
+      auto step = [&](int i, auto par) {
+        constexpr int P = decltype(par)::value;  // i & 1
+        if (i + 2 < nsteps) gload(i + 2, P);     // the set step i was stored from
+        if (active) compute(stage + P * kG128Stage);
+        if (i + 1 < nsteps) sstore(stage + (1 - P) * kG128Stage, 1 - P);
+        __syncthreads();
+      };
+      for (int i = 0; i < nsteps; i += 2) {
+        step(i, std::integral_constant<int, 0>{});
+        if (i + 1 < nsteps) step(i + 1, std::integral_constant<int, 1>{});
+      }
+    } else {
+      if (nsteps > 0) {
+        gload(0, 0);
+        sstore(stage, 0);
+      }
+      __syncthreads();
+      for (int i = 0; i < nsteps; ++i) {
+        const double* cur = n_stages == 2 ? stage + (i & 1) * kG128Stage : stage;
+        const bool more = i + 1 < nsteps;
+        if (more) gload(i + 1, 0);  // in flight during this step's MFMAs
+        if (active) compute(cur);
+        if (n_stages == 1) __syncthreads();  // every wave has read the single stage
+        if (more) sstore(n_stages == 2 ? stage + ((i + 1) & 1) * kG128Stage : stage, 0);
+        __syncthreads();
+      }
     }
     if (active) {
 #pragma unroll
