@@ -56,7 +56,7 @@
 // the large modules' Gram in 128 x 128 workgroup tiles staged through LDS
 // (gram_mfma128); 0: the per-wave 64 x 64 tiles of round 3
 #ifndef NR_BIG_G128
-#define NR_BIG_G128 1
+#define NR_BIG_G128 0  // tuning: 1 = the 128 x 128 LDS-staged workgroup tile (C5 measured 8% slower, profiles/r04/ab7)
 #endif
 
 // Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta.
@@ -333,12 +333,14 @@ struct NetChunk {
 // path and the compiler's wait counts can leave the next chunk's gathers
 // outstanding (PIPE). Table layout (es = 2): the pair's second 16 bytes,
 // {gram, net^T}, sit in the same 32-byte sector as {corr, net}.
-template <int U, bool SYM, bool GRAM>
+// ESC >= 0: the pairs' layout (P.es) fixed at compile time (no per-gather
+// select between the packed and the strided addressing).
+template <int U, bool SYM, bool GRAM, int ESC = -1>
 __device__ __forceinline__ void net_issue(const NetParams& P, const NetLds& L, int64_t k, int64_t cvo,
                                           int64_t npairs, int64_t ch, NetChunk<U>& c) {
   const double2* __restrict__ pairs = P.pairs;
   const int64_t n = P.n_nodes;
-  const int64_t es = P.es;
+  const int64_t es = ESC >= 0 ? ESC : P.es;
   const int64_t v0 = ch * U;
   const int64_t v1 = v0 + U < npairs ? v0 + U : npairs;
   // no discovery vector (observed / vector runs): every x reads the NaN cell
@@ -375,7 +377,11 @@ __device__ __forceinline__ void net_issue(const NetParams& P, const NetLds& L, i
   }
 }
 
-template <int U, bool STORE, bool GRAM>
+// SEG: the column flush by segmented lane scan (wd_flush_column); the
+// two-wave pipelined items (PIPE) flush directly (their lanes mostly share
+// one column, and the scan's dependent shuffles sit on the pipeline's
+// critical path: C5 network launch 38.1 vs 35.2 G reads/s, profiles/r04/ab7).
+template <int U, bool STORE, bool GRAM, bool SEG = NR_WD_SEGSCAN != 0>
 __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L, double* plain_w, int64_t cvo,
                                             double xs, double ys, const NetChunk<U>& c, double* acc,
                                             const GramOut& go, double& g1) {
@@ -439,7 +445,7 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
     }
   }
   // flush the last column of the chunk
-  if (NR_WD_SEGSCAN) {
+  if (SEG) {
     wd_flush_column(L, plain_w, jc, gj, cpl, cff, cpb, con, ctn);
   } else {
     atomicAdd(&plain_w[jc], cpl);
@@ -456,7 +462,7 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
 // Gram is filled from the same gathers -- G_ij for every pair, the diagonal and
 // the ones column here -- into a region the caller zeroed; g1 / bad return
 // this thread's part of 1'G1 over the data block and a non-finite-diagonal flag.
-template <int NW, bool PIPE, bool SYM, bool GRAM = false, int U = 7>
+template <int NW, bool PIPE, bool SYM, bool GRAM = false, int U = 7, int ESC = -1>
 __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_local, int64_t off, int64_t k,
                                          const NetLds& L, const GramOut& go = GramOut{}, double* g1_out = nullptr,
                                          int* bad_out = nullptr) {
@@ -465,7 +471,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   const int wave = tid >> 6;
   const double2* __restrict__ pairs = P.pairs;
   const int64_t n = P.n_nodes;
-  const int64_t es = P.es;
+  const int64_t es = ESC >= 0 ? ESC : P.es;
   double g1 = 0.0;
   int bad = 0;
   // per node: sorted position (SortNodes, src/netStats.cpp:23-32), |diag|,
@@ -515,14 +521,14 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   if (!GRAM && P.cv_out) {  // vector runs (one item per module): CorrVector out, no pipeline
     for (int64_t ch = tid; ch < nchunks; ch += BS) {
       NetChunk<U> c;
-      net_issue<U, SYM, false>(P, L, k, cvo, npairs, ch, c);
+      net_issue<U, SYM, false, ESC>(P, L, k, cvo, npairs, ch, c);
       net_process<U, true, false>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
     }
   } else if (!PIPE) {
     for (int64_t ch = tid; ch < nchunks; ch += BS) {
       NetChunk<U> c;
-      net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch, c);
-      net_process<U, false, GRAM>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
+      net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch, c);
+      net_process<U, false, GRAM, NR_WD_SEGSCAN != 0 && !PIPE>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
     }
   } else if (tid < nchunks) {
     // (no global stores in this loop: pending stores next to the gathers
@@ -533,14 +539,14 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     NetChunk<U> a, b;
     const int64_t last = nchunks - 1;
     int64_t ch = tid;
-    net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch, a);
+    net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch, a);
     for (;;) {
-      net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
-      net_process<U, false, GRAM>(P, L, plain_w, cvo, xs, ys, a, acc, go, g1);
+      net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
+      net_process<U, false, GRAM, NR_WD_SEGSCAN != 0 && !PIPE>(P, L, plain_w, cvo, xs, ys, a, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
-      net_issue<U, SYM, GRAM>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
-      net_process<U, false, GRAM>(P, L, plain_w, cvo, xs, ys, b, acc, go, g1);
+      net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
+      net_process<U, false, GRAM, NR_WD_SEGSCAN != 0 && !PIPE>(P, L, plain_w, cvo, xs, ys, b, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
     }
@@ -608,7 +614,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
 // large for LDS at all -- a persistent grid whose workgroups keep the per-node
 // arrays in their global scratch slot (L2-resident; the atomics go to L2) and
 // loop over the items.
-template <int NW, bool BIG, bool SYM>
+template <int NW, bool BIG, bool SYM, int ESC = -1>
 __global__ void __launch_bounds__(NW * 64)
 module_net_kernel(NetParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -625,7 +631,7 @@ module_net_kernel(NetParams P) {
     if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p_local), P.src.n_null);
     for (int64_t c = threadIdx.x; c < k; c += NW * 64) L.idx[c] = node_index(P.src, key, p_local, off + c);
     __syncthreads();
-    net_item<NW, NW == 2 || BIG, SYM, false, NR_NET_U>(P, m, p_local, off, k, L);
+    net_item<NW, NW == 2 || BIG, SYM, false, NR_NET_U, ESC>(P, m, p_local, off, k, L);
   }
 }
 
@@ -1197,7 +1203,8 @@ __device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
     double ra[2][8], rb[2][8];  // register sets of two K steps (NR_G128_PF == 2 uses both)
-    auto gload = [&](int step, int set) {
+    auto gload = [&](int step, auto setc) {
+      constexpr int set = decltype(setc)::value;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         double* dst = h == 0 ? ra[set] : rb[set];
@@ -1223,7 +1230,8 @@ __device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t
         }
       }
     };
-    auto sstore = [&](double* buf, int set) {
+    auto sstore = [&](double* buf, auto setc) {
+      constexpr int set = decltype(setc)::value;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const double* v = h == 0 ? ra[set] : rb[set];
@@ -1253,38 +1261,40 @@ __device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t
             if (!diag || b >= a) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[a], vb[b], acc[a][b], 0, 0, 0);
       }
     };
-    if (NR_G128_PF == 2 && n_stages == 2) {
+    if constexpr (NR_G128_PF == 2) {  // (the launch guarantees two stages: big_g128_fits)
       // global loads two K steps ahead (register sets alternate), LDS stages one
       // step ahead: a step's operands have two steps of MFMAs (~8,000 cycles)
       // to arrive instead of one
-      if (nsteps > 0) gload(0, 0);
-      if (nsteps > 1) gload(1, 1);
-      if (nsteps > 0) sstore(stage, 0);
+      using C0 = std::integral_constant<int, 0>;
+      using C1 = std::integral_constant<int, 1>;
+      if (nsteps > 0) gload(0, C0{});
+      if (nsteps > 1) gload(1, C1{});
+      if (nsteps > 0) sstore(stage, C0{});
       __syncthreads();
-      auto step = [&](int i, auto par) {
-        constexpr int P = decltype(par)::value;  // i & 1
-        if (i + 2 < nsteps) gload(i + 2, P);     // the set step i was stored from
-        if (active) compute(stage + P * kG128Stage);
-        if (i + 1 < nsteps) sstore(stage + (1 - P) * kG128Stage, 1 - P);
+      auto step = [&](int i, auto par, auto other) {  // par: i & 1
+        if (i + 2 < nsteps) gload(i + 2, par);       // the set step i was stored from
+        if (active) compute(stage + decltype(par)::value * kG128Stage);
+        if (i + 1 < nsteps) sstore(stage + decltype(other)::value * kG128Stage, other);
         __syncthreads();
       };
       for (int i = 0; i < nsteps; i += 2) {
-        step(i, std::integral_constant<int, 0>{});
-        if (i + 1 < nsteps) step(i + 1, std::integral_constant<int, 1>{});
+        step(i, C0{}, C1{});
+        if (i + 1 < nsteps) step(i + 1, C1{}, C0{});
       }
     } else {
+      using C0 = std::integral_constant<int, 0>;
       if (nsteps > 0) {
-        gload(0, 0);
-        sstore(stage, 0);
+        gload(0, C0{});
+        sstore(stage, C0{});
       }
       __syncthreads();
       for (int i = 0; i < nsteps; ++i) {
         const double* cur = n_stages == 2 ? stage + (i & 1) * kG128Stage : stage;
         const bool more = i + 1 < nsteps;
-        if (more) gload(i + 1, 0);  // in flight during this step's MFMAs
+        if (more) gload(i + 1, C0{});  // in flight during this step's MFMAs
         if (active) compute(cur);
         if (n_stages == 1) __syncthreads();  // every wave has read the single stage
-        if (more) sstore(n_stages == 2 ? stage + ((i + 1) & 1) * kG128Stage : stage, 0);
+        if (more) sstore(n_stages == 2 ? stage + ((i + 1) & 1) * kG128Stage : stage, C0{});
         __syncthreads();
       }
     }
@@ -1909,8 +1919,11 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
 // from the Infinity Cache / HBM.
 //
 // SMALLNET: the small class's fused network statistics (P.fused == 2).
+// G128 (with G64): the 128 x 128 workgroup-tile Gram only (the launch checks
+// that the idle vectors hold a stage); a kernel holds one Gram variant, else
+// the compiler merges the variants' MFMA blocks and spills around them.
 template <int NW, bool PACKED, int KB, int MB = 0, bool TABLE = false, bool G64 = false, bool RES = false,
-          bool SMALLNET = false>
+          bool SMALLNET = false, bool G128 = false>
 __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   constexpr int BS = NW * 64;
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
@@ -2024,7 +2037,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       const NetLds NL = carve_net_over<NW>(L.q, L.red, L.idx, kmax);
       double gp = 0.0;
       int bp = 0;
-      net_item<NW, NR_TABLE_PIPE, true, true, NR_TABLE_U>(P.net, m, p_local, off, k, NL, go, &gp, &bp);
+      net_item<NW, NR_TABLE_PIPE, true, true, NR_TABLE_U, 2>(P.net, m, p_local, off, k, NL, go, &gp, &bp);
       g1[0] = gp;
       bad = bp;
       gram_done = true;
@@ -2044,11 +2057,11 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     }
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     if (G64) {
-      // the 128 x 128 workgroup tiles when the idle Lanczos vectors and
-      // partials hold a stage of operand slices (NR_BIG_G128)
+      // the 128 x 128 workgroup tiles: the idle Lanczos vectors and partials
+      // hold one or two stages of operand slices (big_g128_fits)
       const int64_t cap = 6 * (int64_t)kmax + n_part;
-      const int stages = !NR_BIG_G128 ? 0 : cap >= 2 * kG128Stage ? 2 : (cap >= kG128Stage ? 1 : 0);
-      if (NW == 4 && stages > 0) {
+      const int stages = cap >= 2 * kG128Stage ? 2 : 1;
+      if (G128) {
         if (dual)
           gram_mfma128<NW == 4 ? 4 : 4, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad, L.q, stages);
         else
@@ -2119,6 +2132,20 @@ module_profile_packed4_kernel(ProfileParams P) {
 __global__ void __launch_bounds__(NR_BS, 1)
 module_profile_big_kernel(ProfileParams P) {
   profile_body<NR_WAVES, true, 0, 0, false, true>(P);
+}
+
+// The same with the 128 x 128 workgroup-tile Gram (NR_BIG_G128).
+__global__ void __launch_bounds__(NR_BS, 1)
+module_profile_big128_kernel(ProfileParams P) {
+  profile_body<NR_WAVES, true, 0, 0, false, true, false, false, true>(P);
+}
+
+// The idle LDS vectors and partials of the large-module kernel hold a stage of
+// the 128 x 128 tile's operand slices (profile_body's overlay).
+bool big_g128_fits(const ProfileParams& P) {
+  const int kmax = P.kvec > 0 ? P.kvec : P.k_max;
+  return NR_BIG_G128 && NR_WAVES == 4 &&
+         6 * (int64_t)kmax + packed_part_doubles(NR_WAVES, kmax, P.m_max) >= (NR_G128_PF == 2 ? 2 : 1) * kG128Stage;
 }
 
 // The Gram-table launches of the packed class (every item fused, k <= S).
@@ -2469,18 +2496,33 @@ hipError_t launch_net(const NetParams& P0, int64_t n_items, hipStream_t st) {
   P.n_items = n_items;
   if (n_items <= 0) return hipSuccess;
   const size_t lds = net_kernel_lds(P.k_max);
+  // the pairs' layout as a template argument where it is one of the two
+  // plain ones (packed triangle: symmetric only); the Gram table's stride at
+  // run time
+#define NR_NET_LAUNCH(NW_, BIG_, GRID, BLOCK)                                                                \
+  do {                                                                                                      \
+    if (P.symmetric && P.es == 0)                                                                           \
+      hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, true, 0>), GRID, BLOCK, lds, st, P);                 \
+    else if (P.symmetric && P.es == 1)                                                                      \
+      hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, true, 1>), GRID, BLOCK, lds, st, P);                 \
+    else if (P.symmetric)                                                                                   \
+      hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, true, -1>), GRID, BLOCK, lds, st, P);                \
+    else if (P.es == 1)                                                                                     \
+      hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, false, 1>), GRID, BLOCK, lds, st, P);                \
+    else                                                                                                    \
+      hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, false, -1>), GRID, BLOCK, lds, st, P);               \
+  } while (0)
+  if (!P.symmetric && P.es == 0) return hipErrorInvalidValue;  // the packed layout is for symmetric matrices
   if (net_kernel_big(P.k_max)) {
     if (!P.big_scratch || P.big_slots <= 0) return hipErrorInvalidValue;
     const unsigned g = (unsigned)(n_items < P.big_slots ? n_items : P.big_slots);
-    if (P.symmetric) hipLaunchKernelGGL((module_net_kernel<4, true, true>), dim3(g), dim3(256), lds, st, P);
-    else hipLaunchKernelGGL((module_net_kernel<4, true, false>), dim3(g), dim3(256), lds, st, P);
+    NR_NET_LAUNCH(4, true, dim3(g), dim3(256));
   } else if (net_kernel_waves(P.k_max) == 4) {
-    if (P.symmetric) hipLaunchKernelGGL((module_net_kernel<4, false, true>), dim3((unsigned)n_items), dim3(256), lds, st, P);
-    else hipLaunchKernelGGL((module_net_kernel<4, false, false>), dim3((unsigned)n_items), dim3(256), lds, st, P);
+    NR_NET_LAUNCH(4, false, dim3((unsigned)n_items), dim3(256));
   } else {
-    if (P.symmetric) hipLaunchKernelGGL((module_net_kernel<2, false, true>), dim3((unsigned)n_items), dim3(128), lds, st, P);
-    else hipLaunchKernelGGL((module_net_kernel<2, false, false>), dim3((unsigned)n_items), dim3(128), lds, st, P);
+    NR_NET_LAUNCH(2, false, dim3((unsigned)n_items), dim3(128));
   }
+#undef NR_NET_LAUNCH
   return hipGetLastError();
 }
 
@@ -2503,6 +2545,8 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
     }
     else if (packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
       hipLaunchKernelGGL((module_profile_packed4_kernel<kPackedLayoutK, 3>), g, b4, lds, st, P);
+    else if (NR_BIG_G64 && wg_per_cu == 1 && !P.fused && big_g128_fits(P))
+      hipLaunchKernelGGL(module_profile_big128_kernel, g, b4, lds, st, P);
     else if (NR_BIG_G64 && wg_per_cu == 1 && !P.fused)
       hipLaunchKernelGGL(module_profile_big_kernel, g, b4, lds, st, P);
     else
