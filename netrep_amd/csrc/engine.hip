@@ -233,17 +233,14 @@ size_t pair_bytes_of(const nr_ctx* ctx) {
   return ctx->pairs_es == 0 ? n * (n + 1) / 2 * sizeof(double2) : n * n * sizeof(double2) * (size_t)ctx->pairs_es;
 }
 
-// Symmetric matrices of more than 8,192 nodes (a full {corr, net} array
-// beyond 1 GiB) are kept as their packed lower triangle: the network gathers
-// then spread over half the footprint (fewer DRAM pages and translations per
-// gather). Measured (profiles/r04/ab4): C4 (20,000 nodes) 60.3k -> 64.8k
-// perms/s packed; C2 (5,000 nodes, its 400 MB full array mostly in the
-// Infinity Cache) 75.0k full vs 72.1k packed (the triangle's index
-// arithmetic). The rule depends on the shape and the (exact) symmetry only;
-// results are bitwise the same. No memory for the triangle: the full array
-// stays.
+// Tuning option: keep exactly symmetric {corr, net} pairs as their packed
+// lower triangle (half the footprint; results bitwise the same). Measured
+// (profiles/r04/ab4, ab6, ab8) it does not pay with the layout fixed at
+// compile time in the network kernels: C5 (40,000 nodes) 39.7 packed vs 42.0
+// G reads/s full, C4 62.3k vs 62.2k perms/s, C2 72.1k vs 75.0k. Off by
+// default; no memory for the triangle leaves the full array.
 #ifndef NR_PACK_PAIRS
-#define NR_PACK_PAIRS 1  // tuning: 0 never, 1 beyond 8,192 nodes, 2 every symmetric dataset
+#define NR_PACK_PAIRS 0  // tuning: 0 never, 1 beyond 8,192 nodes, 2 every symmetric dataset
 #endif
 int maybe_pack_pairs(nr_ctx* ctx, int64_t n) {
   if (!ctx->symmetric || ctx->pairs_es != 1 || NR_PACK_PAIRS == 0 || n > 65535) return NR_OK;
