@@ -121,22 +121,30 @@ struct NetLds {
   unsigned long long *pb, *on, *tn;  // [k] fixed-point Pb, O; unit count of the rest
   double* ff;                        // [k] the first same-parity term after the diagonal
   int k_stride;
+  // Node i's slot in the per-node arrays: one pad slot per 32 nodes, so the
+  // row targets of one wave instruction (nodes U apart in a column) spread
+  // over all LDS banks (U = 2: a 4-way conflict without it).
+  __device__ __forceinline__ static int at(int i) { return i + (i >> 5); }
 };
+
+// Slots per per-node array (NetLds::at).
+__host__ __device__ __forceinline__ int net_kpad(int kmax) { return kmax + (kmax >> 5) + 1; }
 
 template <int NW>
 __device__ __forceinline__ NetLds carve_net_lds(unsigned char* smem, int kmax) {
   NetLds L;
+  const int kp = net_kpad(kmax);
   L.red = reinterpret_cast<double*>(smem);
   L.plain = L.red + 8 * NW;
-  L.dg = L.plain + (size_t)NW * kmax;
-  L.ff = L.dg + kmax;
-  L.pb = reinterpret_cast<unsigned long long*>(L.ff + kmax);
-  L.on = L.pb + kmax;
-  L.tn = L.on + kmax;
-  L.idx = reinterpret_cast<uint32_t*>(L.tn + kmax);
+  L.dg = L.plain + (size_t)NW * kp;
+  L.ff = L.dg + kp;
+  L.pb = reinterpret_cast<unsigned long long*>(L.ff + kp);
+  L.on = L.pb + kp;
+  L.tn = L.on + kp;
+  L.idx = reinterpret_cast<uint32_t*>(L.tn + kp);
   L.rk = reinterpret_cast<int*>(L.idx + kmax);
-  L.ge = L.rk + kmax;
-  L.k_stride = kmax;
+  L.ge = L.rk + kp;
+  L.k_stride = kp;
   return L;
 }
 
@@ -160,12 +168,14 @@ __device__ __forceinline__ NetLds carve_net_over(double* region, double* red, ui
 }
 
 size_t net_lds_bytes(int nw, int kmax) {
-  return sizeof(double) * (8 * (size_t)nw + (size_t)(nw + 2) * kmax) + sizeof(unsigned long long) * 3 * (size_t)kmax +
-         sizeof(int) * 3 * (size_t)kmax;
+  const size_t kp = (size_t)net_kpad(kmax);
+  return sizeof(double) * (8 * (size_t)nw + (size_t)(nw + 2) * kp) + sizeof(unsigned long long) * 3 * kp +
+         sizeof(int) * ((size_t)kmax + 2 * kp);
 }
 
 // One weighted-degree contribution a = |net(source, target)| (a >= 0).
-__device__ __forceinline__ void wd_add(const NetLds& L, double* plain_w, int t, int pt, int ps, double a) {
+__device__ __forceinline__ void wd_add(const NetLds& L, double* plain_w, int t0, int pt, int ps, double a) {
+  const int t = NetLds::at(t0);
   atomicAdd(&plain_w[t], a);
   const int ge = L.ge[t];
   if (ge == WD_NO_GRID || !isfinite(a)) return;
@@ -213,18 +223,20 @@ __device__ __forceinline__ void wd_flush_column(const NetLds& L, double* plain_w
   const int kn = __shfl_down(jc, 1, 64);
   const bool last = lane == 63 || !((act >> (lane + 1)) & 1ull) || kn != jc;
   if (last) {
-    atomicAdd(&plain_w[jc], cpl);
+    const int t = NetLds::at(jc);
+    atomicAdd(&plain_w[t], cpl);
     if (gj != WD_NO_GRID) {
-      atomicAdd(&L.pb[jc], cpb);
-      atomicAdd(&L.on[jc], con);
-      atomicAdd(&L.tn[jc], ctn);
-      atomicAdd(&L.ff[jc], cff);
+      atomicAdd(&L.pb[t], cpb);
+      atomicAdd(&L.on[t], con);
+      atomicAdd(&L.tn[t], ctn);
+      atomicAdd(&L.ff[t], cff);
     }
   }
 }
 
 // The reference's weighted degree of node c from its accumulated parts.
-__device__ __forceinline__ double wd_final(const NetLds& L, int NWn, int c, int k) {
+__device__ __forceinline__ double wd_final(const NetLds& L, int NWn, int c0, int k) {
+  const int c = NetLds::at(c0);
   double plain = 0.0;
   for (int w = 0; w < NWn; ++w) plain += L.plain[w * L.k_stride + c];
   const double d = L.dg[c];
@@ -387,8 +399,8 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
                                             const GramOut& go, double& g1) {
   // the column's parts, in registers until the column changes
   int jc = c.j0;
-  int pj = L.rk[jc];
-  int gj = L.ge[jc];
+  int pj = L.rk[NetLds::at(jc)];
+  int gj = L.ge[NetLds::at(jc)];
   double cpl = 0.0, cff = 0.0;
   unsigned long long cpb = 0, con = 0, ctn = 0;
 #pragma unroll
@@ -396,18 +408,19 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
     if (c.iis[u] >= 0) {
       const int i = c.iis[u], j = c.jjs[u];
       if (j != jc) {  // the chunk crossed into column j: flush the previous column
-        atomicAdd(&plain_w[jc], cpl);
+        const int t = NetLds::at(jc);
+        atomicAdd(&plain_w[t], cpl);
         if (gj != WD_NO_GRID) {
-          atomicAdd(&L.pb[jc], cpb);
-          atomicAdd(&L.on[jc], con);
-          atomicAdd(&L.tn[jc], ctn);
-          atomicAdd(&L.ff[jc], cff);
+          atomicAdd(&L.pb[t], cpb);
+          atomicAdd(&L.on[t], con);
+          atomicAdd(&L.tn[t], ctn);
+          atomicAdd(&L.ff[t], cff);
         }
         cpl = cff = 0.0;
         cpb = con = ctn = 0;
         jc = j;
-        pj = L.rk[j];
-        gj = L.ge[j];
+        pj = L.rk[NetLds::at(j)];
+        gj = L.ge[NetLds::at(j)];
       }
       const double y = c.e[u].x;
       if (STORE) P.cv_out[cvo + c.v0 + u] = y;
@@ -416,7 +429,7 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
         go.put(pk_at(i, j, go.kc), gv);
         g1 += 2.0 * gv;
       }
-      const int pi = L.rk[i];
+      const int pi = L.rk[NetLds::at(i)];
       // target jj (column idx[jj]) gains row idx[ii]: registers
       const double a = fabs(c.e[u].y);
       cpl += a;
@@ -448,12 +461,13 @@ __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L,
   if (SEG) {
     wd_flush_column(L, plain_w, jc, gj, cpl, cff, cpb, con, ctn);
   } else {
-    atomicAdd(&plain_w[jc], cpl);
+    const int t = NetLds::at(jc);
+    atomicAdd(&plain_w[t], cpl);
     if (gj != WD_NO_GRID) {
-      atomicAdd(&L.pb[jc], cpb);
-      atomicAdd(&L.on[jc], con);
-      atomicAdd(&L.tn[jc], ctn);
-      atomicAdd(&L.ff[jc], cff);
+      atomicAdd(&L.pb[t], cpb);
+      atomicAdd(&L.on[t], con);
+      atomicAdd(&L.tn[t], ctn);
+      atomicAdd(&L.ff[t], cff);
     }
   }
 }
@@ -480,7 +494,8 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     const uint32_t ic = L.idx[c];
     int r = 0;
     for (int64_t c2 = 0; c2 < k; ++c2) r += L.idx[c2] < ic;
-    L.rk[c] = r;
+    const int t = NetLds::at((int)c);
+    L.rk[t] = r;
     const int64_t ad = pair_at(ic, ic, n, es);
     const double d = fabs(pairs[ad].y);
     if (GRAM) {  // G_cc and the ones column's G_kc = sum of column c
@@ -492,14 +507,14 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
       g1 += gcc;
       bad |= (int)!isfinite(gcc);
     }
-    L.dg[c] = d;
-    L.ge[c] = wd_grid_exp(d);
+    L.dg[t] = d;
+    L.ge[t] = wd_grid_exp(d);
 #pragma unroll
-    for (int w = 0; w < NW; ++w) L.plain[w * L.k_stride + c] = 0.0;
-    L.pb[c] = 0;
-    L.on[c] = 0;
-    L.tn[c] = 0;
-    L.ff[c] = 0.0;
+    for (int w = 0; w < NW; ++w) L.plain[w * L.k_stride + t] = 0.0;
+    L.pb[t] = 0;
+    L.on[t] = 0;
+    L.tn[t] = 0;
+    L.ff[t] = 0.0;
   }
   __syncthreads();
 
@@ -556,14 +571,14 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   // Weighted degrees (the reference's rounding, wd_final), into plain[0]:
   // node c's parts are read and overwritten by its owner thread only
   double* wd = L.plain;
-  for (int64_t c = tid; c < k; c += BS) wd[c] = wd_final(L, NW, (int)c, (int)k);
+  for (int64_t c = tid; c < k; c += BS) wd[NetLds::at((int)c)] = wd_final(L, NW, (int)c, (int)k);
   __syncthreads();
 
   // Weighted degree statistics: two-pass over the k values held in LDS.
   const int64_t woff = off;
   double a1[4] = {0, 0, 0, 0};  // sum(all wd), n, sx, sy
   for (int64_t c = tid; c < k; c += BS) {
-    const double y = wd[c];
+    const double y = wd[NetLds::at((int)c)];
     const double xv = P.disc_wd ? P.disc_wd[woff + c] : nr_nan();
     a1[0] += y;
     if (isfinite(xv) && isfinite(y)) {
@@ -576,7 +591,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
   const double mx = a1[2] / a1[1], my = a1[3] / a1[1];
   double a2[3] = {0, 0, 0};
   for (int64_t c = tid; c < k; c += BS) {
-    const double y = wd[c];
+    const double y = wd[NetLds::at((int)c)];
     const double xv = P.disc_wd ? P.disc_wd[woff + c] : nr_nan();
     if (isfinite(xv) && isfinite(y)) {
       const double dx = xv - mx, dy = y - my;
