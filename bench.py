@@ -57,11 +57,25 @@ def _pmc_row(config, batch, kernel, table=False):
             rows = json.load(f)
     except (OSError, ValueError):
         return None
-    for r in rows:
-        if (r.get("config") == config and r.get("batch") == batch and r.get("kernel") == kernel
-                and bool(r.get("gram_table", False)) == table and "superseded" not in r):
+    live = [r for r in rows if r.get("config") == config and r.get("kernel") == kernel
+            and bool(r.get("gram_table", False)) == table and "superseded" not in r]
+    for r in live:
+        if r.get("batch") == batch:
             return r
-    return None
+    # a launch of a nearby size (the reference interface sizes its own
+    # launches, e.g. 66 permutations at C5): the pass's per-launch bytes, flops
+    # and time scaled by the launch size, marked as such
+    near = [r for r in live if r.get("batch") and abs(batch / r["batch"] - 1.0) <= 0.1]
+    if not near:
+        return None
+    r = dict(min(near, key=lambda x: abs(x["batch"] - batch)))
+    f = batch / r["batch"]
+    for key in ("hbm_bytes_per_launch", "fetch_size_kb_raw", "write_size_kb", "avg_ns_rocprof",
+                "mfma_f64_flops_executed"):
+        if key in r:
+            r[key] = r[key] * f
+    r["scaled_from_batch"] = r["batch"]
+    return r
 
 
 def traffic_fields(config, batch, kernel, avg_ms, table=False):
@@ -78,6 +92,8 @@ def traffic_fields(config, batch, kernel, avg_ms, table=False):
     raw = (r["fetch_size_kb_raw"] + r["write_size_kb"]) * 1024.0
     out = {"traffic": float(r["hbm_bytes_per_launch"]), "traffic_range": [raw, float(r["hbm_bytes_per_launch"])],
            "traffic_source": r.get("source"), "traffic_pass_avg_ms": r["avg_ns_rocprof"] / 1e6}
+    if "scaled_from_batch" in r:
+        out["traffic_scaled_from_batch"] = r["scaled_from_batch"]
     if avg_ms > 0:
         out["traffic_time_ratio"] = round(r["avg_ns_rocprof"] / 1e6 / avg_ms, 4)
         # the bytes the kernel actually moves past L2 per second, against HBM peak
