@@ -66,6 +66,23 @@ for it in range(n_items):
         res[b].append(block_steps(G, b))
 ks = np.array(ks, dtype=float)
 w = ks * ks  # a pass costs ~k^2/2 Gram entries
+# Bytes per item (round 4): the Gram passes (packed fp64,
+# k^2/2 x 8 B each) plus the block recurrence's vector traffic with the
+# kernel's partial reorthogonalisation assumed to carry over (every step reads
+# the two previous blocks and writes one, k b doubles each; a full basis pass
+# -- project and update, 2 reads of the basis -- on 8% of the steps, the
+# single-vector kernel's rate: 2.8 per 35 steps). G V on the matrix cores:
+# 2 k^2 b flops per pass, as time at the 78.6 TF/s fp64 peak for C3's 256,000
+# items per launch. LDS: six k-vectors per block column at k = 320.
+base = None
 for b in bs:
     v = np.array(res[b], dtype=float)
-    print(f"b={b:2d}  passes mean {v.mean():6.2f}  max {v.max():4.0f}  k^2-weighted {np.sum(v * w) / w.sum():6.2f}")
+    gram = np.mean(v * ks * ks / 2 * 8)
+    rec = np.mean(v * 3 * ks * b * 8)
+    reo = np.mean(0.08 * v * 2 * ks * (b * v / 2) * 8)
+    tot = gram + rec + reo
+    base = base or tot
+    mfma_ms = np.mean(v * 2 * ks * ks * b) * 256000 / 78.6e12 * 1e3
+    print(f"b={b:2d}  passes mean {v.mean():6.2f}  max {v.max():4.0f}  k^2-weighted {np.sum(v * w) / w.sum():6.2f}  "
+          f"bytes/item: Gram {gram / 1e6:5.2f} MB + recurrence {rec / 1e6:5.2f} + reorth {reo / 1e6:5.2f} "
+          f"= {tot / base:4.2f}x b=1;  G.V at MFMA peak {mfma_ms:5.1f} ms/launch;  LDS vectors {6 * 320 * b * 8 / 1024:5.1f} KB")
