@@ -529,9 +529,6 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
 #define NR_TABLE_G32 1
 #endif
     if (fuse_kind[i] == 1 && !NR_TABLE_G32) seg[i].plan.g32_off = 0;  // tuning: no fp32 copy, no relaxed steps
-#ifndef NR_TABLE_RESIDENT
-#define NR_TABLE_RESIDENT 0  // tuning: 1 = the one-per-CU 8-wave kernel (measured 1.8x slower, profiles/r04/)
-#endif
     if (fuse_kind[i] == 1 && (NR_TABLE_RESIDENT || nr::kTableWaves != nr::kProfileWaves)) {
       int dev_cu = 256;
       (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);

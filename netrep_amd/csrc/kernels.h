@@ -136,6 +136,19 @@ int profile_table_per_cu();
 int64_t profile_table_gram_lds_doubles();
 // The CU-resident Gram-table kernel (one workgroup of kResWaves waves per
 // CU): its LDS carve-out bytes, and the LDS doubles left for the Gram.
+// Tuning options that put a prefix of a table item's packed Gram in LDS
+// (measured slower or equal): the one-per-CU resident
+// kernel (engine.hip launch_profiles) and the LDS prefix of the three-per-CU
+// table kernel. Builds without either compile no LDS branch into the
+// Gram-table stores (GramOut::put).
+#ifndef NR_TABLE_RESIDENT
+#define NR_TABLE_RESIDENT 0
+#endif
+#ifndef NR_TABLE_LDS
+#define NR_TABLE_LDS 0
+#endif
+#define NR_GRAM_LDS (NR_TABLE_RESIDENT || NR_TABLE_LDS)
+
 #ifndef NR_RES_WAVES
 #define NR_RES_WAVES 8
 #endif

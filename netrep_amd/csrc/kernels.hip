@@ -317,12 +317,14 @@ struct GramOut {
   double* lds = nullptr;  // the resident kernel: packed entries below lds_n live in LDS (fp64 only)
   int64_t lds_n = 0;
   __device__ __forceinline__ void put(int64_t a, double v) const {
+#if NR_GRAM_LDS
     if (a < lds_n) {
       lds[a] = v;
-    } else {
-      G[a] = v;
-      if (G32) G32[a] = (float)v;
+      return;
     }
+#endif
+    G[a] = v;
+    if (G32) G32[a] = (float)v;
   }
 };
 
@@ -2167,9 +2169,6 @@ bool big_g128_fits(const ProfileParams& P) {
 #ifndef NR_TABLE_KERNEL
 #define NR_TABLE_KERNEL 1
 #endif
-#ifndef NR_TABLE_LDS
-#define NR_TABLE_LDS 0  // tuning: 1 = an LDS prefix of the Gram in the three-per-CU table kernel
-#endif
 __global__ void __launch_bounds__(kTableWaves * 64, 3)
 module_profile_table_kernel(ProfileParams P) {
   profile_body<kTableWaves, true, kPackedLayoutK, 0, true, false, NR_TABLE_LDS != 0>(P);
@@ -2549,7 +2548,7 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
     // the compile-time layout of modules of <= 320 nodes at three workgroups
     // per CU (measured fastest: profiles/r02/profile_variants.txt), else the
     // runtime layout
-    if (P.fused == 1 && P.lds_gram_n > 0 && packed_bucket(P.k_max) == kPackedLayoutK)
+    if (NR_TABLE_RESIDENT && P.fused == 1 && P.lds_gram_n > 0 && packed_bucket(P.k_max) == kPackedLayoutK)
       hipLaunchKernelGGL(module_profile_resident_kernel, g, dim3(64 * kResWaves),
                          profile_resident_carve() + sizeof(double) * (size_t)P.lds_gram_n, st, P);
     else if (NR_TABLE_KERNEL && P.fused == 1 && packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3) {
