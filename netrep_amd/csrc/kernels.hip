@@ -199,26 +199,52 @@ __device__ __forceinline__ void wd_add(const NetLds& L, double* plain_w, int t0,
 // active lower lane. The fixed-point parts are integers (exact in any order);
 // the plain sums stay per wave in a fixed order (deterministic); the first
 // same-parity term after the diagonal is one term per node.
-#ifndef NR_WD_SEGSCAN
-#define NR_WD_SEGSCAN 1
-#endif
+// One step of the segmented scan: the values of the lane DPP control CTRL
+// names (row_shr:s within 16-lane rows, row_bcast:15 / :31 across rows; rows
+// outside ROWMASK and lanes without a source keep the identity) are added
+// where that lane's column equals this one's. DPP moves are VALU operations:
+// no LDS instruction and no LDS round trip on the flush's dependency chain
+// (the __shfl_up form issued 66 ds_bpermute per flush).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int wd_dpp_i32(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ unsigned long long wd_dpp_u64(unsigned long long v) {
+  const int lo = wd_dpp_i32<CTRL, ROWMASK>(0, (int)(unsigned)v);
+  const int hi = wd_dpp_i32<CTRL, ROWMASK>(0, (int)(unsigned)(v >> 32));
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void wd_scan_step(int jc, double& cpl, double& cff, unsigned long long& cpb,
+                                             unsigned long long& con, unsigned long long& ctn) {
+  const int ko = wd_dpp_i32<CTRL, ROWMASK>(-1, jc);
+  const double a0 = __builtin_bit_cast(double, wd_dpp_u64<CTRL, ROWMASK>(__builtin_bit_cast(unsigned long long, cpl)));
+  const double a1 = __builtin_bit_cast(double, wd_dpp_u64<CTRL, ROWMASK>(__builtin_bit_cast(unsigned long long, cff)));
+  const unsigned long long b0 = wd_dpp_u64<CTRL, ROWMASK>(cpb), b1 = wd_dpp_u64<CTRL, ROWMASK>(con),
+                           b2 = wd_dpp_u64<CTRL, ROWMASK>(ctn);
+  if (ko == jc) {
+    cpl += a0;
+    cff += a1;
+    cpb += b0;
+    con += b1;
+    ctn += b2;
+  }
+}
+
 __device__ __forceinline__ void wd_flush_column(const NetLds& L, double* plain_w, int jc, int gj, double cpl,
                                                 double cff, unsigned long long cpb, unsigned long long con,
                                                 unsigned long long ctn) {
   const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int ko = __shfl_up(jc, o, 64);
-    const double a0 = __shfl_up(cpl, o, 64), a1 = __shfl_up(cff, o, 64);
-    const unsigned long long b0 = __shfl_up(cpb, o, 64), b1 = __shfl_up(con, o, 64), b2 = __shfl_up(ctn, o, 64);
-    if (lane >= o && ko == jc) {
-      cpl += a0;
-      cff += a1;
-      cpb += b0;
-      con += b1;
-      ctn += b2;
-    }
-  }
+  // Hillis-Steele within rows (the columns are non-decreasing with the lane,
+  // so a matching key at distance s means the whole span matches), then the
+  // rows' last lanes across rows
+  wd_scan_step<0x111, 0xF>(jc, cpl, cff, cpb, con, ctn);  // row_shr:1
+  wd_scan_step<0x112, 0xF>(jc, cpl, cff, cpb, con, ctn);  // row_shr:2
+  wd_scan_step<0x114, 0xF>(jc, cpl, cff, cpb, con, ctn);  // row_shr:4
+  wd_scan_step<0x118, 0xF>(jc, cpl, cff, cpb, con, ctn);  // row_shr:8
+  wd_scan_step<0x142, 0xA>(jc, cpl, cff, cpb, con, ctn);  // row_bcast:15 into rows 1, 3
+  wd_scan_step<0x143, 0xC>(jc, cpl, cff, cpb, con, ctn);  // row_bcast:31 into rows 2, 3
   const unsigned long long act = __ballot(1);
   const int kn = __shfl_down(jc, 1, 64);
   const bool last = lane == 63 || !((act >> (lane + 1)) & 1ull) || kn != jc;
@@ -395,7 +421,7 @@ __device__ __forceinline__ void net_issue(const NetParams& P, const NetLds& L, i
 // two-wave pipelined items (PIPE) flush directly (their lanes mostly share
 // one column, and the scan's dependent shuffles sit on the pipeline's
 // critical path: C5 network launch 38.1 vs 35.2 G reads/s, profiles/r04/ab7).
-template <int U, bool STORE, bool GRAM, bool SEG = NR_WD_SEGSCAN != 0>
+template <int U, bool STORE, bool GRAM, bool SEG = true>
 __device__ __forceinline__ void net_process(const NetParams& P, const NetLds& L, double* plain_w, int64_t cvo,
                                             double xs, double ys, const NetChunk<U>& c, double* acc,
                                             const GramOut& go, double& g1) {
@@ -545,7 +571,7 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     for (int64_t ch = tid; ch < nchunks; ch += BS) {
       NetChunk<U> c;
       net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch, c);
-      net_process<U, false, GRAM, NR_WD_SEGSCAN != 0 && !PIPE>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
+      net_process<U, false, GRAM, !PIPE>(P, L, plain_w, cvo, xs, ys, c, acc, go, g1);
     }
   } else if (tid < nchunks) {
     // (no global stores in this loop: pending stores next to the gathers
@@ -559,11 +585,11 @@ __device__ __forceinline__ void net_item(const NetParams& P, int m, int64_t p_lo
     net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch, a);
     for (;;) {
       net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, b);
-      net_process<U, false, GRAM, NR_WD_SEGSCAN != 0 && !PIPE>(P, L, plain_w, cvo, xs, ys, a, acc, go, g1);
+      net_process<U, false, GRAM, !PIPE>(P, L, plain_w, cvo, xs, ys, a, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
       net_issue<U, SYM, GRAM, ESC>(P, L, k, cvo, npairs, ch + BS < last ? ch + BS : last, a);
-      net_process<U, false, GRAM, NR_WD_SEGSCAN != 0 && !PIPE>(P, L, plain_w, cvo, xs, ys, b, acc, go, g1);
+      net_process<U, false, GRAM, !PIPE>(P, L, plain_w, cvo, xs, ys, b, acc, go, g1);
       ch += BS;
       if (ch >= nchunks) break;
     }
