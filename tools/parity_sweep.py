@@ -6,7 +6,7 @@ largest and the 99.9th-percentile scaled error |gpu - oracle| /
 max(|oracle|, 1e-2), NA-pattern agreement, and the p-value identity record
 (tests/conftest.assert_pvalues_identical) over the whole sample.
 
-  python tools/parity_sweep.py [C3 perms] [C2 perms] > out.json
+  python tools/parity_sweep.py [C3 perms] [C2 perms] [C5 perms] > out.json
 
 Test infrastructure (the oracle is the checker here, never the product)."""
 import json
@@ -65,7 +65,14 @@ def sweep(cfg, seed, n_perm, chunk):
 def main():
     n3 = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     n2 = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
-    out = {"C3": sweep("C3", 0x5EED, n3, 256), "C2": sweep("C2", 0xC2C2, n2, 512)}
+    n5 = int(sys.argv[3]) if len(sys.argv) > 3 else 0   # C5 (k up to 2,000 > S = 1,000): large-module kernels
+    out = {}
+    if n3 > 0:
+        out["C3"] = sweep("C3", 0x5EED, n3, 256)
+    if n2 > 0:
+        out["C2"] = sweep("C2", 0xC2C2, n2, 512)
+    if n5 > 0:
+        out["C5"] = sweep("C5", 0xC5C5, n5, 32)
     print(json.dumps(out, indent=1))
 
 
