@@ -733,6 +733,10 @@ def main():
                        "perms_per_step": P, "launch_batch": B, "global_perms": total_perms,
                        "parallelism": f"perm-shard x{world}"},
             "module_perms_per_sec": value * len(lay.modules),
+            # the Gram table's one-off build (first, untimed run) charged to
+            # this run's timed region: what `value` would be with it inside
+            "value_incl_table_build": (total_perms / (elapsed + eng.gram_table_ms() / 1e3)
+                                       if table else None),
             "algorithmic_GBps": value * (net_b + prof_b) / 1e9,
             "roofline": roofline,
             "kernels": kernels,

@@ -93,10 +93,10 @@ def test_bench_traffic_lookup_matches_committed_pmc():
     assert bench.traffic_fields("C2", 256, "module_profile_kernel", 1.0)["traffic"] is None
     # a launch within 10% of a pass's size (the reference interface's own
     # launches, 66 permutations at C5): the pass scaled by the size, marked
+    t66 = bench.traffic_fields("C5", 66, "module_profile_kernel", 50.0)   # the final-tree pass
     t64 = bench.traffic_fields("C5", 64, "module_profile_kernel", 50.0)
-    t66 = bench.traffic_fields("C5", 66, "module_profile_kernel", 50.0)
-    assert "traffic_scaled_from_batch" not in t64 and t66["traffic_scaled_from_batch"] == 64
-    assert abs(t66["traffic"] / t64["traffic"] - 66 / 64) < 1e-12
+    assert "traffic_scaled_from_batch" not in t66 and t64["traffic_scaled_from_batch"] == 66
+    assert abs(t64["traffic"] / t66["traffic"] - 64 / 66) < 1e-12
 
 
 def test_vars_present_aligned_by_label_from_contingency():
