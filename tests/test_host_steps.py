@@ -93,10 +93,11 @@ def test_bench_traffic_lookup_matches_committed_pmc():
     assert bench.traffic_fields("C2", 256, "module_profile_kernel", 1.0)["traffic"] is None
     # a launch within 10% of a pass's size (the reference interface's own
     # launches, 66 permutations at C5): the pass scaled by the size, marked
-    t66 = bench.traffic_fields("C5", 66, "module_profile_kernel", 50.0)   # the final-tree pass
-    t64 = bench.traffic_fields("C5", 64, "module_profile_kernel", 50.0)
-    assert "traffic_scaled_from_batch" not in t66 and t64["traffic_scaled_from_batch"] == 66
-    assert abs(t64["traffic"] / t66["traffic"] - 64 / 66) < 1e-12
+    t66 = bench.traffic_fields("C5", 66, "module_profile_kernel", 50.0)   # the three-dataset pass
+    t70 = bench.traffic_fields("C5", 70, "module_profile_kernel", 50.0)
+    assert "traffic_scaled_from_batch" not in t66 and t70["traffic_scaled_from_batch"] == 66
+    assert abs(t70["traffic"] / t66["traffic"] - 70 / 66) < 1e-12
+    assert bench.traffic_fields("C5", 80, "module_profile_kernel", 50.0)["traffic"] is None  # > 10% off
 
 
 def test_vars_present_aligned_by_label_from_contingency():
