@@ -227,6 +227,9 @@ int nr_set_batch(nr_ctx* ctx, int64_t perms_per_launch);
  * The reference-interface calls set their contexts' count from n_cores and
  * never change the process default. */
 int nr_set_host_threads(int n);
+/* The process-wide default set by nr_set_host_threads (pooled contexts are
+ * reset to it when a reference-interface call returns them). */
+int nr_get_host_threads(void);
 int nr_ctx_set_host_threads(nr_ctx* ctx, int n);
 /* Host -> device bytes the library has copied since it was loaded (every
  * upload path counts): a caller can verify that resident data is not

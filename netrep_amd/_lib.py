@@ -112,6 +112,7 @@ SIGNATURES = {
     "netrep_set_progress_hook": (None, [C.c_void_p, C.c_void_p]),
     "netrep_format_progress": (_int, [_i64, _i64, C.c_char_p, _i64]),
     "nr_set_host_threads": (_int, [_int]),
+    "nr_get_host_threads": (_int, []),
     "netrep_PrefetchTestDataset": (_int, [_dp, _dp, _dp, _i64, _i64]),
     "nr_set_dataset_files": (_int, [_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
                                     C.c_char_p, _int]),

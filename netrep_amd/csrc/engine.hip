@@ -18,6 +18,7 @@
 #include <mutex>
 #include <thread>
 #include <string>
+#include <set>
 #include <vector>
 
 #include "../../include/netrep_gpu.h"
@@ -109,10 +110,6 @@ struct nr_ctx {
   double* h_stage2 = nullptr;
   size_t stage2_cap = 0;
   hipEvent_t ev_copy[2] = {nullptr, nullptr};
-  // NR_NET_SIDE: the network launch on a stream of its own beside the
-  // profile launches (per lane: main, observed), forked/joined by events
-  hipStream_t net_stream[2] = {nullptr, nullptr};
-  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
 
   // The observed statistics' own lane (nr_observed_async): stream, scratch and
   // work queue, so that they run beside the first permutation batch instead
@@ -230,36 +227,7 @@ int n_stat_of(const nr_ctx* ctx) { return ctx->d_data ? NR_NSTAT_DATA : NR_NSTAT
 // Bytes of the resident {corr, net} array in its layout (pairs_es).
 size_t pair_bytes_of(const nr_ctx* ctx) {
   const size_t n = (size_t)ctx->n_nodes;
-  return ctx->pairs_es == 0 ? n * (n + 1) / 2 * sizeof(double2) : n * n * sizeof(double2) * (size_t)ctx->pairs_es;
-}
-
-// Tuning option: keep exactly symmetric {corr, net} pairs as their packed
-// lower triangle (half the footprint; results bitwise the same). Measured
-// (profiles/r04/ab4, ab6, ab8) it does not pay with the layout fixed at
-// compile time in the network kernels: C5 (40,000 nodes) 39.7 packed vs 42.0
-// G reads/s full, C4 62.3k vs 62.2k perms/s, C2 72.1k vs 75.0k. Off by
-// default; no memory for the triangle leaves the full array.
-#ifndef NR_PACK_PAIRS
-#define NR_PACK_PAIRS 0  // tuning: 0 never, 1 beyond 8,192 nodes, 2 every symmetric dataset
-#endif
-int maybe_pack_pairs(nr_ctx* ctx, int64_t n) {
-  if (!ctx->symmetric || ctx->pairs_es != 1 || NR_PACK_PAIRS == 0 || n > 65535) return NR_OK;
-  if (NR_PACK_PAIRS == 1 && n <= 8192) return NR_OK;
-  double2* tri = nullptr;
-  if (hipMalloc((void**)&tri, (size_t)(n * (n + 1) / 2) * sizeof(double2)) != hipSuccess) {
-    (void)hipGetLastError();
-    return NR_OK;
-  }
-  hipError_t e = nr::launch_pack_pairs(ctx->d_pairs, tri, n, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  if (e != hipSuccess) {
-    (void)hipFree(tri);
-    return hip_fail(ctx, e, "pack pairs");
-  }
-  dfree(ctx->d_pairs);
-  ctx->d_pairs = tri;
-  ctx->pairs_es = 0;
-  return NR_OK;
+  return n * n * sizeof(double2) * (size_t)ctx->pairs_es;
 }
 
 // No dataset: buffers freed, shape zero. Modules validated against an earlier
@@ -366,10 +334,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   // the dual (S x S) Gram of modules with k > S: the Gram side is min(k, S),
   // and so is every Lanczos dimension (basis columns of that length)
   plan->k_gram = std::min(k_max, n_samples);
-#ifndef NR_SMALL_CLASS
-#define NR_SMALL_CLASS 1
-#endif
-  if (NR_SMALL_CLASS && plan->k_gram <= nr::kSmallDim) {
+  if (plan->k_gram <= nr::kSmallDim) {
     // the small class (kernels.h): several small-workgroup items per CU;
     // modules longer than its LDS vectors keep their per-node arrays in the
     // slot's scratch
@@ -391,9 +356,6 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   plan->m = mg;
   int kvec = k_max;
   plan->big = false;
-#ifndef NR_PACKED_BIG
-#define NR_PACKED_BIG 1
-#endif
   if (nr::profile_kernel_lds(kvec, mg, n_samples, 2) > 160 * 1024) {
     // Large modules on the packed Gram too (half the Lanczos bytes of the
     // full ld x ld Gram): LDS vectors as long as fit, and the per-node arrays
@@ -401,7 +363,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
     // Lanczos dimension min(k, S) fits the vectors.
     int kp = (k_max + 15) / 16 * 16;
     while (kp > 16 && nr::profile_kernel_lds(kp, mg, n_samples, 2) > 160 * 1024) kp -= 16;
-    if (NR_PACKED_BIG && plan->k_gram <= kp) {
+    if (plan->k_gram <= kp) {
       kvec = kp;
       plan->big = k_max > kp;
     } else {
@@ -430,10 +392,7 @@ int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, Profile
   const size_t lds = nr::profile_kernel_lds(kvec, mg, n_samples, variant);
   if (lds > 160 * 1024)
     return fail(ctx, NR_ERR_UNSUPPORTED, "module too large for the summary-profile kernel's LDS budget");
-#ifndef NR_BIG_ALWAYS
-#define NR_BIG_ALWAYS 0  // tuning: every packed launch beyond the 320-node layout on the large-module kernel
-#endif
-  const int want = variant == 4 || variant == 6 || (NR_BIG_ALWAYS && variant == 2 && k_max > nr::kPackedLayoutK) ? 1 : 3;
+  const int want = variant == 4 || variant == 6 ? 1 : 3;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(want, (160 * 1024) / lds));
   plan->variant = variant;
   plan->per_cu = per_cu;
@@ -519,23 +478,8 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     const bool fuse_table = table_np && table_np->es == 2 && seg[i].plan.variant == 2 &&
                             k_max <= nr::kPackedLayoutK && k_max <= pp.n_samples &&
                             nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
-    // the small class computes its items' network statistics from the
-    // {corr, net} pairs itself (symmetric matrices; launch_batch passes the
-    // pairs only then)
-    const bool fuse_small = table_np && table_np->es == 1 && seg[i].plan.variant == 5 && i == ns - 1;
-    fuse_kind[i] = fuse_table ? 1 : fuse_small ? 2 : 0;
+    fuse_kind[i] = fuse_table ? 1 : 0;
     fuse[i] = fuse_kind[i] != 0;
-#ifndef NR_TABLE_G32
-#define NR_TABLE_G32 1
-#endif
-    if (fuse_kind[i] == 1 && !NR_TABLE_G32) seg[i].plan.g32_off = 0;  // tuning: no fp32 copy, no relaxed steps
-    if (fuse_kind[i] == 1 && (NR_TABLE_RESIDENT || nr::kTableWaves != nr::kProfileWaves)) {
-      int dev_cu = 256;
-      (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-      seg[i].plan.per_cu = NR_TABLE_RESIDENT ? 1 : nr::profile_table_per_cu();
-      seg[i].plan.slots = (int)std::max<int64_t>(
-          1, std::min<int64_t>((int64_t)seg[i].count * n_perm, (int64_t)dev_cu * seg[i].plan.per_cu));
-    }
     total = std::max<int64_t>(total, seg[i].plan.stride * seg[i].plan.slots);
   }
   // segments run one after the other on one stream: they share the scratch
@@ -555,23 +499,10 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.scratch_stride = plan.stride;
     pp.part_global = plan.variant == 4 || plan.variant == 6 ? 1 : 0;
     pp.vec_global = plan.variant == 6 ? 1 : 0;
-#ifndef NR_ORDER
-#define NR_ORDER 0  // tuning: 0 the cache-budget rule, 1 always module-major, 2 always permutation-major
-#endif
-    pp.order_tail = NR_ORDER == 1 ? 0
-                    : NR_ORDER == 2 ? (int)std::min<int64_t>(n_perm - 1, (plan.slots + seg[i].count - 1) / seg[i].count)
-                                    : profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm,
-                                                         (int)pp.n_samples);
+    pp.order_tail =
+        profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples);
     pp.g32_off = plan.g32_off;
     pp.fused = fuse_kind[i];
-    pp.lds_gram_n = 0;
-    if (pp.fused == 1 && NR_TABLE_RESIDENT) {
-      // the CU-resident kernel: one workgroup per CU, the Gram's leading units
-      // in LDS; permutation-major order keeps a size mix in flight, so the
-      // rest of the Grams (the slots' scratch) stays in the XCDs' L2
-      pp.lds_gram_n = nr::profile_resident_gram_doubles();
-      pp.order_tail = (int)std::min<int64_t>(n_perm - 1, (plan.slots + seg[i].count - 1) / seg[i].count);
-    }
     if (pp.fused) {
       pp.net = *table_np;
       pp.net.mod_order = pp.mod_order;
@@ -661,10 +592,6 @@ int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std
   return NR_OK;
 }
 
-#ifndef NR_NET_SIDE
-#define NR_NET_SIDE 0  // tuning: 1 = the unfused network launch on a side stream, concurrent with the profiles
-#endif
-
 // Launch the statistics kernels for n_perm permutations (or the observed /
 // direct sets when src.mode == NR_IDX_DIRECT, n_perm == 1) into d_out.
 int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double* d_out, const Lane& ln) {
@@ -708,9 +635,6 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   // phase fused into the profile items without the table at +0.7%, within
   // run-to-run noise, and on a concurrent stream at -11%.)
   const bool table = data && ctx->pairs_es == 2;
-  // the small class's launch computes its own items' network statistics
-  // (fused == 2) for symmetric matrices
-  const bool small_fuse = data && !table && ctx->symmetric && nr::small_fuse_enabled();
   auto nets = [&](int n_mod) -> int {
     if (n_mod <= 0) return NR_OK;
     std::vector<int32_t> ks(ctx->order_k_h.begin(), ctx->order_k_h.begin() + n_mod);
@@ -719,29 +643,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     if (ln.timed) timer_end(ctx, 0, (int64_t)n_mod * n_perm, ln.st);
     return NR_OK;
   };
-  // NR_NET_SIDE: without fusion the network launch runs on the lane's side
-  // stream concurrently with the profile launches (both only write their own
-  // statistic rows of d_out, after fill_na); the lane's stream joins it.
-  const bool side = NR_NET_SIDE && data && !table && !small_fuse;
-  if (side) {
-    const int id = ln.id;
-    if (!ctx->net_stream[id]) {
-      NR_HIP(ctx, hipStreamCreateWithFlags(&ctx->net_stream[id], hipStreamNonBlocking));
-      NR_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork[id], hipEventDisableTiming));
-      NR_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join[id], hipEventDisableTiming));
-    }
-    NR_HIP(ctx, hipEventRecord(ctx->ev_fork[id], ln.st));
-    NR_HIP(ctx, hipStreamWaitEvent(ctx->net_stream[id], ctx->ev_fork[id], 0));
-    Lane sl = ln;
-    sl.st = ctx->net_stream[id];
-    std::vector<int32_t> ks(ctx->order_k_h.begin(), ctx->order_k_h.begin() + ctx->n_present);
-    if (sl.timed) timer_begin(ctx, 0, sl.st);
-    if ((rc = launch_nets(ctx, np, ctx->d_mod_order, ks, n_perm, sl))) return rc;
-    if (sl.timed) timer_end(ctx, 0, (int64_t)ctx->n_present * n_perm, sl.st);
-    NR_HIP(ctx, hipEventRecord(ctx->ev_join[id], sl.st));
-  } else if (!table && !small_fuse && (rc = nets(ctx->n_present))) {
-    return rc;
-  }
+  if (!table && (rc = nets(ctx->n_present))) return rc;
 
   if (data) {
     nr::ProfileParams pp{};
@@ -764,13 +666,12 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     pp.stamps = ln.timed ? ctx->d_stamps : nullptr;
     int fused_from = ctx->n_present;
     if (ln.timed) timer_begin(ctx, 1, ln.st);
-    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ln,
-                         table || small_fuse ? &np : nullptr, &fused_from);
+    rc = launch_profiles(ctx, pp, ctx->d_mod_order, ctx->order_k_h, n_perm, ln, table ? &np : nullptr,
+                         &fused_from);
     if (rc) return rc;
     if (ln.timed) timer_end(ctx, 1, n_items, ln.st);
-    if ((table || small_fuse) && (rc = nets(fused_from))) return rc;
+    if (table && (rc = nets(fused_from))) return rc;
   }
-  if (side) NR_HIP(ctx, hipStreamWaitEvent(ln.st, ctx->ev_join[ln.id], 0));
   if (ln.timed) timer_collect(ctx);
   return NR_OK;
 }
@@ -810,6 +711,15 @@ bool table_wanted(nr_ctx* ctx) {
     }
   }
   if (packed_max == 0 || packed_max > S || packed_w < 0.5 * total_w) return false;
+  // A fixed per-device bound, not the free memory (the numerical
+  // path must not depend on what else holds the device): the build's peak,
+  // 56 bytes per matrix element (the {corr, net} pairs, the Gram and the
+  // widened table), within 60% of the device's total HBM.
+  {
+    size_t total = 0;
+    if (hipDeviceTotalMem(&total, ctx->device) != hipSuccess) return false;
+    if ((double)n * (double)n * 56.0 > 0.6 * (double)total) return false;
+  }
   ProfilePlan plan;
   if (plan_profile(ctx, 1, packed_max, (int)S, &plan) != NR_OK) return false;
   return plan.variant == 2 &&
@@ -833,11 +743,8 @@ int maybe_build_table(nr_ctx* ctx) {
     dfree(tab);
     dfree(cs);
   };
-#ifndef NR_TABLE_ALLOC
-#define NR_TABLE_ALLOC 0  // tuning: the table's allocation flags (hipExtMallocWithFlags; 3 = uncached)
-#endif
   if (hipMalloc((void**)&gram, nn * sizeof(double)) != hipSuccess ||
-      hipExtMallocWithFlags((void**)&tab, 2 * nn * sizeof(double2), NR_TABLE_ALLOC) != hipSuccess ||
+      hipMalloc((void**)&tab, 2 * nn * sizeof(double2)) != hipSuccess ||
       hipMalloc((void**)&cs, (size_t)n * sizeof(double)) != hipSuccess) {
     drop();
     (void)hipGetLastError();
@@ -849,7 +756,7 @@ int maybe_build_table(nr_ctx* ctx) {
   }
   hipError_t e = nr::launch_gram_full(ctx->d_data, S, n, gram, cs, ctx->stream);
   if (e == hipSuccess)
-    e = nr::launch_widen_pairs(ctx->d_pairs, gram, tab, n, ctx->symmetric, ctx->pairs_es == 0, ctx->stream);
+    e = nr::launch_widen_pairs(ctx->d_pairs, gram, tab, n, ctx->symmetric, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     drop();
@@ -1125,11 +1032,6 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   for (auto& ev : ctx->ev_copy)
     if (ev) (void)hipEventDestroy(ev);
   if (ctx->obs_stream) (void)hipStreamDestroy(ctx->obs_stream);
-  for (int i = 0; i < 2; ++i) {
-    if (ctx->net_stream[i]) (void)hipStreamDestroy(ctx->net_stream[i]);
-    if (ctx->ev_fork[i]) (void)hipEventDestroy(ctx->ev_fork[i]);
-    if (ctx->ev_join[i]) (void)hipEventDestroy(ctx->ev_join[i]);
-  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1145,6 +1047,8 @@ int nr_set_host_threads(int n) {
   g_host_threads = n <= 0 ? 8 : std::min(n, 16);
   return NR_OK;
 }
+
+int nr_get_host_threads(void) { return g_host_threads.load(); }
 
 int nr_ctx_set_host_threads(nr_ctx* ctx, int n) {
   if (!ctx) return NR_ERR_INVALID;
@@ -1295,7 +1199,6 @@ int set_dataset_impl(nr_ctx* ctx, const double* corr, const double* net, const d
   ctx->symmetric = (asym & 1) ? 0 : 1;
   ctx->corr_finite = (asym & 2) ? 0 : 1;
   ctx->net_finite = (asym & 4) ? 0 : 1;
-  if (int rc = maybe_pack_pairs(ctx, n_nodes)) return rc;
   ctx->n_nodes = n_nodes;
   ctx->n_samples = data ? n_samples : 0;
   return NR_OK;
@@ -1409,7 +1312,6 @@ int set_dataset_files_impl(nr_ctx* ctx, const char* corr_path, const char* net_p
   ctx->symmetric = (asym & 1) ? 0 : 1;
   ctx->corr_finite = (asym & 2) ? 0 : 1;
   ctx->net_finite = (asym & 4) ? 0 : 1;
-  if ((rc = maybe_pack_pairs(ctx, n_nodes))) return rc;
   // committed only once everything above has succeeded
   ctx->node_names = names;
   ctx->n_nodes = n_nodes;
@@ -1506,6 +1408,36 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
 // fan-out (each destination pulls all B over its one link to the source) or
 // a single pipelined ring (DESIGN.md section 7 has the arithmetic). The source
 // must be idle; on failure every destination is left with no dataset.
+// Peer access between every pair of distinct GPUs a broadcast uses, in both
+// directions (the scatter reads GPU 0 from each destination's stream, the
+// all-gather reads every destination from every other): direct copies over
+// the xGMI links instead of copies staged through host memory
+// (src/permutations.cpp:335-380 is the reference's one-process parallel
+// section this replaces). Enabled once per ordered pair per process; a pair
+// without peer access is an error, not a silent host-staged copy.
+static std::mutex g_peer_mu;
+static std::set<std::pair<int, int>> g_peer_on;
+
+static int enable_peer_access(nr_ctx* err_ctx, const std::vector<int>& devs) {
+  std::lock_guard<std::mutex> lk(g_peer_mu);
+  for (int a : devs)
+    for (int b : devs) {
+      if (a == b || g_peer_on.count({a, b})) continue;
+      int can = 0;
+      NR_HIP(err_ctx, hipDeviceCanAccessPeer(&can, a, b));
+      if (!can)
+        return fail(err_ctx, NR_ERR_HIP,
+                    "GPU " + std::to_string(a) + " cannot access GPU " + std::to_string(b) +
+                        " as a peer (no xGMI path): the dataset broadcast needs peer access");
+      NR_HIP(err_ctx, hipSetDevice(a));
+      const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return hip_fail(err_ctx, e, "hipDeviceEnablePeerAccess");
+      (void)hipGetLastError();  // clears hipErrorPeerAccessAlreadyEnabled
+      g_peer_on.insert({a, b});
+    }
+  return NR_OK;
+}
+
 int nr_broadcast_dataset(nr_ctx* const* ctxs, int n) {
   if (!ctxs || n < 1) return NR_ERR_INVALID;
   nr_ctx* src = ctxs[0];
@@ -1515,6 +1447,12 @@ int nr_broadcast_dataset(nr_ctx* const* ctxs, int n) {
       if (!ctxs[g] || ctxs[g] == ctxs[h]) return fail(src, NR_ERR_INVALID, "broadcast: contexts must be distinct");
   if (!src->d_pairs) return fail(src, NR_ERR_INVALID, "source context has no dataset");
   if (n == 1) return NR_OK;
+  {
+    std::vector<int> devs;
+    for (int g = 0; g < n; ++g)
+      if (std::find(devs.begin(), devs.end(), ctxs[g]->device) == devs.end()) devs.push_back(ctxs[g]->device);
+    if (int rc = enable_peer_access(src, devs)) return rc;
+  }
   const int parts = n - 1;
   struct Buf {
     const char* s;
@@ -1623,6 +1561,7 @@ int nr_clear_dataset(nr_ctx* ctx) {
   NR_HIP(ctx, hipSetDevice(ctx->device));
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
   reset_dataset(ctx);
+  ctx->cancel = false;  // a context cancelled after its run returned starts clean
   return NR_OK;
 }
 

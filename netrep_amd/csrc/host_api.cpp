@@ -123,7 +123,12 @@ void give_ctx(CtxPtr& c) {
   if (!c) return;
   std::lock_guard<std::mutex> lk(g_pool_mu);
   auto it = g_ctx_device.find(c.get());
-  if (it == g_ctx_device.end() || g_pool.size() >= kPoolMax || nr_clear_dataset(c.get()) != NR_OK) {
+  // nr_clear_dataset also clears a pending cancellation (the
+  // progress monitor cancels every context of a call, including ones whose
+  // run had already returned); the host-thread count goes back to the
+  // process default, so the next call's staging does not inherit nCores
+  if (it == g_ctx_device.end() || g_pool.size() >= kPoolMax || nr_clear_dataset(c.get()) != NR_OK ||
+      nr_ctx_set_host_threads(c.get(), nr_get_host_threads()) != NR_OK) {
     if (it != g_ctx_device.end()) g_ctx_device.erase(it);
     c.reset();
     return;
@@ -140,19 +145,40 @@ struct CtxLease {
 };
 
 // A dataset kept resident between calls that name the same host arrays: the
-// pointers and shape must match, and so must a fingerprint of 1,024 sampled
-// elements of each array (evenly spread, both ends included) -- a freed and
-// reused address with other contents is not mistaken for the same matrix.
+// pointers and shape must match, and so must a fingerprint of EVERY element of
+// each array (a sampled fingerprint missed in-place edits between
+// the sample points, and R's temporaries reuse freed addresses). One host pass
+// at memory bandwidth, split over the process's staging threads; each element
+// is mixed with its position, so a changed, moved or swapped element changes
+// the sum (a 64-bit sum of position-keyed multiplicative mixes).
+uint64_t fp_chunk(const double* a, int64_t i0, int64_t i1) {
+  uint64_t h = 0;
+  for (int64_t i = i0; i < i1; ++i) {
+    uint64_t b;
+    std::memcpy(&b, a + i, 8);
+    uint64_t x = b ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    h += x;
+  }
+  return h;
+}
 uint64_t fingerprint(const double* a, int64_t n) {
   uint64_t h = 0x243F6A8885A308D3ull ^ (uint64_t)n;
   if (!a || n <= 0) return h;
-  const int64_t k = std::min<int64_t>(n, 1024);
-  for (int64_t i = 0; i < k; ++i) {
-    const int64_t pos = k > 1 ? i * (n - 1) / (k - 1) : 0;
-    uint64_t b;
-    std::memcpy(&b, a + pos, 8);
-    h ^= b + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-  }
+  const int64_t per = 1 << 22;  // 32 MiB per task
+  const int nt = (int)std::min<int64_t>(std::max(1, nr_get_host_threads()), (n + per - 1) / per);
+  std::vector<uint64_t> part((size_t)nt, 0);
+  auto body = [&](int t) {
+    const int64_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+    part[(size_t)t] = fp_chunk(a, i0, i1);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(body, t);
+  body(0);
+  for (auto& x : th) x.join();
+  for (uint64_t v : part) h += v;
   return h;
 }
 
@@ -610,9 +636,20 @@ int netrep_PermutationProcedure(const netrep_disc_props* disc, const double* t_d
     return set_err(NR_ERR_INVALID, "invalid arguments to PermutationProcedure");
   // a dataset uploaded ahead (netrep_PrefetchTestDataset) is adopted
   CtxPtr pre = take_prefetch(t_data, t_corr, t_net, n_samples, n_nodes);
-  return permutation_impl(disc, t_data != nullptr, t_data, t_corr, t_net, n_samples, n_nodes, t_names, ma_names,
+  int rc = permutation_impl(disc, t_data != nullptr, t_data, t_corr, t_net, n_samples, n_nodes, t_names, ma_names,
+                            ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose, seed, pi,
+                            nulls_out, observed_out, std::move(pre), n_cores);
+  // Device memory held between calls (resident discovery / NetProps datasets,
+  // pending prefetches, pooled contexts' scratch) must not turn a run that
+  // fits the device into NR_ERR_OOM: release all of it and try
+  // once more from the host matrices. The numerical path does not change.
+  if (rc == NR_ERR_OOM) {
+    netrep_ReleaseResident();
+    rc = permutation_impl(disc, t_data != nullptr, t_data, t_corr, t_net, n_samples, n_nodes, t_names, ma_names,
                           ma_labels, n_assign, modules, n_modules, n_perm, null_hypothesis, verbose, seed, pi,
-                          nulls_out, observed_out, std::move(pre), n_cores);
+                          nulls_out, observed_out, CtxPtr(), n_cores);
+  }
+  return rc;
 } catch (const std::bad_alloc&) {
   return set_err(NR_ERR_OOM, "host memory allocation failed");
 } catch (const std::exception& e) {

@@ -18,10 +18,7 @@ constexpr int NR_N_STAMPS = 16;
 // CU in flight instead of three 4-wave items); per-node arrays of modules
 // longer than kSmallDim in the slot's scratch.
 constexpr int kSmallDim = 112;
-#ifndef NR_SMALL_WAVES
-#define NR_SMALL_WAVES 2
-#endif
-constexpr int kSmallWaves = NR_SMALL_WAVES;
+constexpr int kSmallWaves = 2;  // (one wave per item measured slower: profiles/r03/small_class/)
 
 // Where the test column of module node c comes from.
 struct IndexSource {
@@ -37,9 +34,8 @@ struct IndexSource {
 
 struct NetParams {
   const double2* pairs;        // interleaved {corr, net}, column-major n x n (es = 1), or the
-                               // Gram table: {corr, net}, {gram, net^T} per (i, j) (es = 2), or the
-                               // packed lower triangle of symmetric matrices (es = 0)
-  int32_t es;                  // element stride of pairs in double2 units (1 or 2; 0: packed)
+                               // Gram table: {corr, net}, {gram, net^T} per (i, j) (es = 2)
+  int32_t es;                  // element stride of pairs in double2 units (1 or 2)
   const double* colsum;        // [n_nodes] column sums of the data (Gram table only)
   int64_t n_nodes;
   int symmetric;               // both matrices exactly symmetric
@@ -107,10 +103,8 @@ struct ProfileParams {
   // Gram table (packed kernel only): the network statistics of each item are
   // computed in the profile workgroup from one gather per pair of the table,
   // which also fills the item's packed Gram (no matrix-core Gram for k <= S)
-  int32_t fused;                // 1: Gram-table items (network statistics + Gram from the table);
-                               // 2: the small class with its network statistics in the same workgroup
+  int32_t fused;                // 1: Gram-table items (network statistics + Gram from the table)
   NetParams net;
-  int64_t lds_gram_n;          // resident kernel: LDS doubles for the Gram's leading units (0: not resident)
 };
 
 size_t net_kernel_lds(int k_max);
@@ -124,37 +118,11 @@ hipError_t launch_net(const NetParams& P, int64_t n_items, hipStream_t st);
 // Whether the packed kernel's LDS (vectors of kvec, basis mmax) holds the
 // network item's per-node arrays (the fused Gram-table path).
 bool fused_net_fits(int kvec, int mmax, int nw);
-// waves per workgroup of the Gram-table kernel (tuning option NR_TABLE_WAVES),
-// its LDS bytes and workgroups per CU
-#ifndef NR_TABLE_WAVES
-#define NR_TABLE_WAVES 4
-#endif
-constexpr int kTableWaves = NR_TABLE_WAVES;
+// waves per workgroup of the Gram-table kernel (2 waves x 5 per CU measured
+// 13% slower, profiles/r03/table_waves/), its LDS bytes and workgroups per CU
+constexpr int kTableWaves = 4;
 size_t profile_table_lds();
 int profile_table_per_cu();
-// LDS doubles the table kernel keeps for its item's Gram prefix (NR_TABLE_LDS)
-int64_t profile_table_gram_lds_doubles();
-// The CU-resident Gram-table kernel (one workgroup of kResWaves waves per
-// CU): its LDS carve-out bytes, and the LDS doubles left for the Gram.
-// Tuning options that put a prefix of a table item's packed Gram in LDS
-// (measured slower or equal): the one-per-CU resident
-// kernel (engine.hip launch_profiles) and the LDS prefix of the three-per-CU
-// table kernel. Builds without either compile no LDS branch into the
-// Gram-table stores (GramOut::put).
-#ifndef NR_TABLE_RESIDENT
-#define NR_TABLE_RESIDENT 0
-#endif
-#ifndef NR_TABLE_LDS
-#define NR_TABLE_LDS 0
-#endif
-#define NR_GRAM_LDS (NR_TABLE_RESIDENT || NR_TABLE_LDS)
-
-#ifndef NR_RES_WAVES
-#define NR_RES_WAVES 8
-#endif
-constexpr int kResWaves = NR_RES_WAVES;
-size_t profile_resident_carve();
-int64_t profile_resident_gram_doubles();
 // The Gram table of a dataset with data: gram[i + j n] = x_i . x_j over the
 // n_samples rows of X (n_samples x (n + 2), the virtual columns behind), and
 // colsum[j] = sum of column j.
@@ -162,16 +130,10 @@ hipError_t launch_gram_full(const double* X, int64_t S, int64_t n, double* gram,
 // {corr, net} pairs (es = 1) + gram -> the table layout (es = 2):
 // out[2e] = in[e], out[2e + 1] = {gram[e], net(j, i)} for e = i + j n.
 hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* out, int64_t n, int symmetric,
-                              int packed, hipStream_t st);
-// full n x n {corr, net} pairs -> the packed lower triangle (es = 0; symmetric matrices only)
-hipError_t launch_pack_pairs(const double2* in, double2* out, int64_t n, hipStream_t st);
+                              hipStream_t st);
 // the small class (variant 5): its LDS bytes per workgroup and workgroups per CU
 size_t profile_small_lds();
 int profile_small_per_cu();
-// whether the small class computes its items' network statistics itself (NR_SMALL_FUSE),
-// and its LDS bytes per workgroup then (the network arrays of k_max-node modules)
-bool small_fuse_enabled();
-size_t small_fused_lds(int k_max);
 // variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch,
 // 5 the small class, 6 full Gram with the partials and every vector in scratch
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,

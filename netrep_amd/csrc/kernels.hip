@@ -26,43 +26,16 @@
 // (C3 shape, profiles/r03/table_gathers/): 7 pairs 15.86 ms per 256
 // permutations, 5: 15.07, 4: 14.73, 3: 14.41-14.56, 2: 14.27, 1: 14.87; the
 // next chunk in flight adds at most 0.4% (2 pairs: 14.21) for more spill.
-#ifndef NR_TABLE_U
 #define NR_TABLE_U 2
-#endif
-#ifndef NR_TABLE_PIPE
 #define NR_TABLE_PIPE false
-#endif
-
-// the network kernel's gathers: pairs per chunk
-#ifndef NR_NET_U
+// the network kernel's gathers: pairs per chunk (3/4/7 measured, profiles/r03/net_chunk/)
 #define NR_NET_U 7
-#endif
-// the small class's fused network statistics: pairs per chunk (its 168-VGPR budget)
-#ifndef NR_SMALL_NET_U
-#define NR_SMALL_NET_U 2
-#endif
-
-// units in flight per wave in the packed matvec's fp64 passes
-#ifndef NR_MV_UF64
+// units in flight per wave in the packed matvec's fp64 passes (2 measured
+// slower, profiles/r03/matvec_uf/)
 #define NR_MV_UF64 1
-#endif
-
-// the large modules' 64 x 64 Gram: prefetched step in a second register set
-// used in turn (1) or copied (0)
-#ifndef NR_G64_PINGPONG
-#define NR_G64_PINGPONG 0
-#endif
-
-// the large modules' Gram in 128 x 128 workgroup tiles staged through LDS
-// (gram_mfma128); 0: the per-wave 64 x 64 tiles of round 3
-#ifndef NR_BIG_G128
-#define NR_BIG_G128 0  // tuning: 1 = the 128 x 128 LDS-staged workgroup tile (C5 measured 8% slower, profiles/r04/ab7)
-#endif
-
-// Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta.
-#ifndef NR_LZ_TOL
+// Lanczos stop rule: top Ritz residual <= NR_LZ_TOL * theta (DESIGN.md section 5;
+// 5e-14 measured 2.9% faster at twice the worst statistic difference)
 #define NR_LZ_TOL 5e-15
-#endif
 
 namespace nr {
 
@@ -303,15 +276,10 @@ __device__ __forceinline__ double wd_final(const NetLds& L, int NWn, int c0, int
 // through its LDS work -- with two waves per CU nothing else hides it.
 // ---------------------------------------------------------------------------
 // Element (r, c) of the resident {corr, net} pairs: column-major n x n with
-// element stride es (1 = pairs, 2 = the Gram table), or es = 0, the packed
-// lower triangle of symmetric matrices (column j holds rows j..n-1 from offset
-// j n - j (j - 1) / 2; engine.hip pack rule).
-__host__ __device__ __forceinline__ int64_t tri_at(int64_t r, int64_t c, int64_t n) {
-  const int64_t i = r > c ? r : c, j = r > c ? c : r;
-  return j * n - j * (j - 1) / 2 + (i - j);
-}
+// element stride es (1 = pairs, 2 = the Gram table). (A packed lower triangle
+// of symmetric matrices measured equal or slower, profiles/r04/ab8/.)
 __device__ __forceinline__ int64_t pair_at(int64_t r, int64_t c, int64_t n, int64_t es) {
-  return es == 0 ? tri_at(r, c, n) : (r + c * n) * es;
+  return (r + c * n) * es;
 }
 
 // a global (not constant) cell, so the discovery-load pointer stays a global pointer
@@ -339,15 +307,7 @@ struct GramOut {
   float* G32;
   int kc;
   double S;
-  double* lds = nullptr;  // the resident kernel: packed entries below lds_n live in LDS (fp64 only)
-  int64_t lds_n = 0;
   __device__ __forceinline__ void put(int64_t a, double v) const {
-#if NR_GRAM_LDS
-    if (a < lds_n) {
-      lds[a] = v;
-      return;
-    }
-#endif
     G[a] = v;
     if (G32) G32[a] = (float)v;
   }
@@ -1093,23 +1053,15 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
         }
       };
       if (full > 0) ld16(0, cur);
-      if (NR_G64_PINGPONG) {  // two register sets in turn (no copy of the prefetched step)
-        for (int s0 = 0; s0 < full; s0 += 32) {
-          if (s0 + 16 < full) ld16(s0 + 16, nxt);
-          mfma64(cur);
-          if (s0 + 16 >= full) break;
-          if (s0 + 32 < full) ld16(s0 + 32, cur);
-          mfma64(nxt);
-        }
-      } else {
-        for (int s0 = 0; s0 < full; s0 += 16) {
-          if (s0 + 16 < full) ld16(s0 + 16, nxt);
-          mfma64(cur);
+      // the prefetched step copied into the current set (two register sets
+      // used in turn spilled more: profiles/r03/big_gram64/)
+      for (int s0 = 0; s0 < full; s0 += 16) {
+        if (s0 + 16 < full) ld16(s0 + 16, nxt);
+        mfma64(cur);
 #pragma unroll
-          for (int o = 0; o < 8; ++o)
+        for (int o = 0; o < 8; ++o)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
-        }
+          for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
       }
       if (full < S) {  // the last, partial step
 #pragma unroll
@@ -1150,23 +1102,13 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
         }
       };
       load(4 * kk, cur);
-      if (NR_G64_PINGPONG) {  // two register sets in turn (no copy of the prefetched step)
-        for (int c0 = 0; c0 < k; c0 += 32) {
-          if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
-          mfma64(cur);
-          if (c0 + 16 >= k) break;
-          if (c0 + 32 < k) load(c0 + 32 + 4 * kk, cur);
-          mfma64(nxt);
-        }
-      } else {
-        for (int c0 = 0; c0 < k; c0 += 16) {
-          if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
-          mfma64(cur);
+      for (int c0 = 0; c0 < k; c0 += 16) {
+        if (c0 + 16 < k) load(c0 + 16 + 4 * kk, nxt);
+        mfma64(cur);
 #pragma unroll
-          for (int o = 0; o < 8; ++o)
+        for (int o = 0; o < 8; ++o)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
-        }
+          for (int q = 0; q < 4; ++q) cur[o][q] = nxt[o][q];
       }
     }
 #pragma unroll
@@ -1191,178 +1133,6 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
           }
         }
       }
-  }
-}
-
-// 128 x 128 workgroup tiles of the large modules' Gram (primal [X 1]^T[X 1]
-// or the dual H of k > S), four waves as 2 x 2 sub-tiles of 64 x 64 (each
-// the 4 x 4 MFMA tiles of gram_mfma64, same K order within a 16-step and
-// the same epilogue). Each 16-deep K step of the tile's two operand slices
-// (128 columns x 16 each) is loaded from global once per workgroup into LDS
-// and read by the waves that share it: half the operand traffic of
-// gram_mfma64's independent per-wave tiles, which made the large items'
-// Gram operand-bound at ~55% of the MFMA peak (C5).
-// The staging overlays the Lanczos vectors and matvec partials (idle until
-// the Lanczos phase; the caller zeroes the partials again), double-buffered
-// when they hold two stages (one barrier per K step), else single-buffered.
-// Row stride 132 doubles: the two K rows a ds_read_b64 lane group reads (4
-// rows apart) fall on disjoint bank halves.
-#ifndef NR_G128_PF
-#define NR_G128_PF 2  // global-load distance in K steps (1: the next step only)
-#endif
-constexpr int kG128Ld = 132;
-constexpr int kG128Stage = 2 * 16 * kG128Ld;  // doubles of one stage (A and B slices)
-
-template <int NW, bool DUAL>
-__device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t* idx, int k, int64_t ones_off,
-                             double* __restrict__ G, float* __restrict__ G32, double& g1sum, int& bad,
-                             double* stage, int n_stages) {
-  static_assert(NW == 4, "2 x 2 waves per 128 x 128 tile");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wa = wave >> 1, wb = wave & 1;
-  const int i16 = lane & 15, kk = lane >> 4;
-  const int kc = DUAL ? S + 1 : k + 1;
-  const int T4 = (kc + 63) / 64;
-  const int T8 = (kc + 127) / 128;
-  const int nsup = T8 * (T8 + 1) / 2;
-  const int kdim = DUAL ? k : S;  // contraction length
-  const int nsteps = (kdim + 15) / 16;
-  // one thread's share of a K step: 8 consecutive elements of one operand
-  // column, for the row slice (A, rows of I8) and the column slice (B, J8)
-  const int gr = DUAL ? (tid & 15) * 8 : tid >> 1;  // tile row (first of 8 for DUAL)
-  const int gk = DUAL ? tid >> 4 : (tid & 1) * 8;   // K row (first of 8 for primal)
-  for (int t = 0; t < nsup; ++t) {
-    int I8 = 0, rem = t;
-    while (rem >= T8 - I8) { rem -= T8 - I8; ++I8; }
-    const int J8 = I8 + rem;
-    const int I4 = 2 * I8 + wa, J4 = 2 * J8 + wb;
-    const bool active = I4 <= J4 && J4 < T4;  // uniform over the wave
-    const bool diag = I4 == J4;
-    nr_f64x4 acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
-    double ra[2][8], rb[2][8];  // register sets of two K steps (NR_G128_PF == 2 uses both)
-    auto gload = [&](int step, auto setc) {
-      constexpr int set = decltype(setc)::value;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        double* dst = h == 0 ? ra[set] : rb[set];
-        const int base = 128 * (h == 0 ? I8 : J8);
-        if (DUAL) {
-          const int c = 16 * step + gk;  // node
-          const bool valid = c < k;
-          const double* colp = X + (int64_t)idx[valid ? c : k - 1] * S;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int sm = base + gr + e;  // sample
-            const double x = sm < S ? colp[sm] : (sm == S ? 1.0 : 0.0);
-            dst[e] = valid ? x : 0.0;
-          }
-        } else {
-          const int c = base + gr;  // node (k: the ones column, beyond: the zero column)
-          const double* colp = X + (c < k ? (int64_t)idx[c] * S : (c == k ? ones_off : ones_off + S));
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int sm = 16 * step + gk + e;
-            dst[e] = sm < S ? colp[sm] : 0.0;
-          }
-        }
-      }
-    };
-    auto sstore = [&](double* buf, auto setc) {
-      constexpr int set = decltype(setc)::value;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const double* v = h == 0 ? ra[set] : rb[set];
-        double* sl = buf + h * 16 * kG128Ld;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (DUAL) sl[gk * kG128Ld + gr + e] = v[e];
-          else sl[(gk + e) * kG128Ld + gr] = v[e];
-        }
-      }
-    };
-    auto compute = [&](const double* buf) {
-      const double* sa = buf;
-      const double* sb = buf + 16 * kG128Ld;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int kr = 4 * kk + q;  // gram_mfma64's K order within the step
-        double va[4], vb[4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) va[a] = sa[kr * kG128Ld + 64 * wa + 16 * a + i16];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) vb[b] = sb[kr * kG128Ld + 64 * wb + 16 * b + i16];
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b)
-            if (!diag || b >= a) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(va[a], vb[b], acc[a][b], 0, 0, 0);
-      }
-    };
-    if constexpr (NR_G128_PF == 2) {  // (the launch guarantees two stages: big_g128_fits)
-      // global loads two K steps ahead (register sets alternate), LDS stages one
-      // step ahead: a step's operands have two steps of MFMAs (~8,000 cycles)
-      // to arrive instead of one
-      using C0 = std::integral_constant<int, 0>;
-      using C1 = std::integral_constant<int, 1>;
-      if (nsteps > 0) gload(0, C0{});
-      if (nsteps > 1) gload(1, C1{});
-      if (nsteps > 0) sstore(stage, C0{});
-      __syncthreads();
-      auto step = [&](int i, auto par, auto other) {  // par: i & 1
-        if (i + 2 < nsteps) gload(i + 2, par);       // the set step i was stored from
-        if (active) compute(stage + decltype(par)::value * kG128Stage);
-        if (i + 1 < nsteps) sstore(stage + decltype(other)::value * kG128Stage, other);
-        __syncthreads();
-      };
-      for (int i = 0; i < nsteps; i += 2) {
-        step(i, C0{}, C1{});
-        if (i + 1 < nsteps) step(i + 1, C1{}, C0{});
-      }
-    } else {
-      using C0 = std::integral_constant<int, 0>;
-      if (nsteps > 0) {
-        gload(0, C0{});
-        sstore(stage, C0{});
-      }
-      __syncthreads();
-      for (int i = 0; i < nsteps; ++i) {
-        const double* cur = n_stages == 2 ? stage + (i & 1) * kG128Stage : stage;
-        const bool more = i + 1 < nsteps;
-        if (more) gload(i + 1, C0{});  // in flight during this step's MFMAs
-        if (active) compute(cur);
-        if (n_stages == 1) __syncthreads();  // every wave has read the single stage
-        if (more) sstore(n_stages == 2 ? stage + ((i + 1) & 1) * kG128Stage : stage, C0{});
-        __syncthreads();
-      }
-    }
-    if (active) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          if (diag && b < a) continue;
-          pk_store_tile16(G, G32, kc, 4 * I4 + a, 4 * J4 + b, acc[a][b], lane);
-          const double wgt = (diag && a == b) ? 1.0 : 2.0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            // D[row = (lane>>4) + 4r][col = lane & 15] (f64 MFMA C/D map)
-            const int gi = (4 * I4 + a) * 16 + kk + 4 * r;
-            const int gj = (4 * J4 + b) * 16 + i16;
-            const double val = acc[a][b][r];
-            if (DUAL) {
-              if (gj == S && gi < S) g1sum += val * val;  // |X 1|^2 from the row sums
-              if (gi == gj && gi < S) bad |= (int)!isfinite(val);
-            } else {
-              if (gi < k && gj < k) g1sum += wgt * val;
-              if (gi == gj && gi < k) bad |= (int)!isfinite(val);
-            }
-          }
-        }
-    }
   }
 }
 
@@ -1463,15 +1233,10 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
 //
 // SQ: out_r = sum_c G_rc^2 over c < k instead (squared row norms of the
 // leading k x k block, for start_column; x and y unused).
-//
-// RES: the units below lds_n (a prefix in address order, whole units) are
-// read from the item's LDS copy `lds` (fp64; rounded to fp32 in the relaxed
-// passes, as the global copy would give them), the rest from global scratch.
-template <int NW, bool F32 = false, bool SQ = false, bool RES = false>
+template <int NW, bool F32 = false, bool SQ = false>
 __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int kc, int k, const double* x,
                                                  double* out, double* part, int ks,
-                                                 const double* y, double* red,
-                                                 const double* lds = nullptr, int64_t lds_n = 0) {
+                                                 const double* y, double* red) {
   constexpr int EB = F32 ? 4 : 8;  // element bytes
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1508,23 +1273,15 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
         const bool valid = u + i < u1;
         const int h = min(64, P - 16 * lcg - 64 * lj);
         const int64_t base = pk_base(lcg, P) + 1024 * (int64_t)lj;
-        if (RES && valid && base + 16 * h <= lds_n) {  // an LDS-resident unit (uniform over the wave)
-          // relaxed passes round it to fp32 exactly as the global fp32 copy
-          // holds it: the pass is bitwise the non-resident one
-          const double* lp = lds + base + lane;
+        const int vo = valid && lane < h ? lane * EB : (int)0x80000000;
+        int so = valid ? (int)base * EB : 0;
 #pragma unroll
-          for (int t = 0; t < 16; ++t) gb[i][t] = (LT)(lane < h ? lp[t * h] : 0.0);
-        } else {
-          const int vo = valid && lane < h ? lane * EB : (int)0x80000000;
-          int so = valid ? (int)base * EB : 0;
-#pragma unroll
-          for (int t = 0; t < 16; ++t) {
-            if (F32)
-              gb[i][t] = (LT)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo, so, 0));
-            else
-              gb[i][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
-            so += h * EB;
-          }
+        for (int t = 0; t < 16; ++t) {
+          if (F32)
+            gb[i][t] = (LT)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo, so, 0));
+          else
+            gb[i][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
+          so += h * EB;
         }
         if (++lj == ((P - 16 * lcg + 63) >> 6)) {
           ++lcg;
@@ -1604,16 +1361,15 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
 // summation order, ties to the smaller index). q <- G e_c* (fp64); cn: n
 // doubles of LDS work space. Returns false (q untouched) if every column is
 // zero. Ends with a barrier.
-template <int NW, bool RES = false>
+template <int NW>
 __device__ __forceinline__ bool start_column(const double* __restrict__ G, const float* __restrict__ G32, int kc,
-                                             int n, double* q, double* cn, double* part, int ks, double* red,
-                                             const double* lds = nullptr, int64_t lds_n = 0) {
+                                             int n, double* q, double* cn, double* part, int ks, double* red) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (G32)
-    packed_matvec<NW, true, true, RES>(G32, kc, n, nullptr, cn, part, ks, nullptr, red, lds, lds_n);
+    packed_matvec<NW, true, true>(G32, kc, n, nullptr, cn, part, ks, nullptr, red);
   else
-    packed_matvec<NW, false, true, RES>(G, kc, n, nullptr, cn, part, ks, nullptr, red, lds, lds_n);
+    packed_matvec<NW, false, true>(G, kc, n, nullptr, cn, part, ks, nullptr, red);
   __syncthreads();
   double best = -1.0;
   int bi = 0x7fffffff;
@@ -1653,7 +1409,7 @@ __device__ __forceinline__ bool start_column(const double* __restrict__ G, const
   if (ok)
     for (int r = tid; r < n; r += BS) {
       const int64_t a = pk_at(r > bi ? r : bi, r > bi ? bi : r, kc);
-      q[r] = RES && a < lds_n ? lds[a] : G[a];
+      q[r] = G[a];
     }
   __syncthreads();  // q published; red free again
   return ok;
@@ -1954,18 +1710,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
 // TABLE: a launch whose items all take the Gram-table path (P.fused, no dual
 // items): the matrix-core and dual Gram code is not compiled in, which lowers
 // the register demand of the kernel (its spills at the 168-VGPR budget).
-// RES: the CU-resident Gram-table kernel (one workgroup per CU): the item's
-// packed Gram lives in LDS as far as P.lds_gram_n doubles reach (a prefix of
-// whole matvec units), the rest in the slot's scratch, which at one item per
-// CU stays mostly in the XCD's L2 -- the matvecs stop re-streaming the Gram
-// from the Infinity Cache / HBM.
-//
-// SMALLNET: the small class's fused network statistics (P.fused == 2).
-// G128 (with G64): the 128 x 128 workgroup-tile Gram only (the launch checks
-// that the idle vectors hold a stage); a kernel holds one Gram variant, else
-// the compiler merges the variants' MFMA blocks and spills around them.
-template <int NW, bool PACKED, int KB, int MB = 0, bool TABLE = false, bool G64 = false, bool RES = false,
-          bool SMALLNET = false, bool G128 = false>
+// G64: the large modules' 64 x 64 per-wave super-tile Gram (one workgroup per
+// CU); a kernel holds one Gram variant, else the compiler merges the
+// variants' MFMA blocks and spills around them.
+template <int NW, bool PACKED, int KB, int MB = 0, bool TABLE = false, bool G64 = false>
 __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   constexpr int BS = NW * 64;
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
@@ -2000,10 +1748,6 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   double* gnode = Q + P.basis_doubles + (pglob ? (int64_t)NW * kmax : 0);
   const double* __restrict__ X = P.data;
   const double Sd = (double)S;
-  // the resident kernel's LDS Gram region: behind the carve-out (idx is its last array)
-  double* const glds = RES ? reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(L.idx) +
-                                                       ((sizeof(uint32_t) * kmax + 15) & ~(size_t)15))
-                           : nullptr;
 
   if (PACKED) {  // the matvec's partial arrays start zero (packed_matvec keeps them so)
     for (int i = tid; i < n_part; i += BS) part[i] = 0.0;
@@ -2029,35 +1773,14 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     double g1[1] = {0.0};
     int bad = 0;
     bool gram_done = false;
-    // resident kernel: the LDS prefix of this item's packed Gram (whole units)
-    int64_t lds_n = 0;
-    if (RES) {
-      const int Pp = kc;
-      for (int g = 0; 16 * g < Pp; ++g) {
-        bool full = false;
-        for (int r0 = 16 * g; r0 < Pp; r0 += 64) {
-          const int h = min(64, Pp - r0);
-          if (lds_n + 16 * h > P.lds_gram_n) {
-            full = true;
-            break;
-          }
-          lds_n += 16 * h;
-        }
-        if (full) break;
-      }
-    }
-    auto gl = [&](int64_t a) -> double { return RES && a < lds_n ? glds[a] : G[a]; };
+    auto gl = [&](int64_t a) -> double { return G[a]; };
     if (TABLE || (PACKED && P.fused == 1 && !dual)) {
       // Gram table: the item's network statistics from one 32-byte gather per
       // pair, which also carries G_ij -- the packed Gram is filled here (into
       // a zeroed region: padding and the diagonal blocks' upper parts stay 0)
       // and the matrix-core Gram is skipped. The per-node arrays live in the
       // Lanczos vectors' LDS, idle until the Lanczos phase.
-      GramOut go{G, G32, kc, Sd};
-      if (RES) {
-        go.lds = glds;
-        go.lds_n = lds_n;
-      }
+      const GramOut go{G, G32, kc, Sd};
       {
         // The fill below writes every lower-triangle entry over kc = k + 1
         // (pairs, diagonal, ones column); zero only what it never writes: the
@@ -2081,36 +1804,13 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       bad = bp;
       gram_done = true;
       for (int64_t i = tid; i < n_part; i += BS) part[i] = 0.0;  // the per-node arrays overlapped them
-    } else if (SMALLNET && P.fused == 2) {
-      // the small class (C2): the item's network statistics in the same
-      // workgroup, from the {corr, net} pairs (symmetric matrices), before
-      // its matrix-core Gram -- no separate network launch; the gathers wait
-      // while the CU's other items run their Lanczos steps. The per-node
-      // arrays overlay the Lanczos carve-out from L.q on (the launch sizes the
-      // LDS for k_max: small_fused_lds); a module beyond the LDS vectors keeps
-      // its index set in the slot's scratch, so the overlay may cover L.idx.
-      const NetLds NL = carve_net_over<NW>(L.q, L.red, idx_p, k <= kmax ? kmax : P.k_max);
-      net_item<NW, false, true, false, NR_SMALL_NET_U>(P.net, m, p_local, off, k, NL);
-      for (int64_t i = tid; i < n_part; i += BS) part[i] = 0.0;
-      __syncthreads();
     }
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     if (G64) {
-      // the 128 x 128 workgroup tiles: the idle Lanczos vectors and partials
-      // hold one or two stages of operand slices (big_g128_fits)
-      const int64_t cap = 6 * (int64_t)kmax + n_part;
-      const int stages = cap >= 2 * kG128Stage ? 2 : 1;
-      if (G128) {
-        if (dual)
-          gram_mfma128<NW == 4 ? 4 : 4, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad, L.q, stages);
-        else
-          gram_mfma128<NW == 4 ? 4 : 4, false>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad, L.q, stages);
-        for (int64_t i = tid; i < n_part; i += BS) part[i] = 0.0;  // the staging overlapped them
-      } else if (dual) {
+      if (dual)
         gram_mfma64<NW, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
-      } else {
+      else
         gram_mfma64<NW, false>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad);
-      }
     } else if (!TABLE) {
       if (dual)
         gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
@@ -2127,10 +1827,10 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       bool relax = false;
       auto mv = [&](const double* x, double* out, const double* y) -> double {
         if (!PACKED) return matvec(G, ld, n, x, out, part, kmax, y, L.red);
-        return relax ? packed_matvec<NW, true, false, RES>(G32, kc, n, x, out, part, kmax, y, L.red, glds, lds_n)
-                     : packed_matvec<NW, false, false, RES>(G, kc, n, x, out, part, kmax, y, L.red, glds, lds_n);
+        return relax ? packed_matvec<NW, true, false>(G32, kc, n, x, out, part, kmax, y, L.red)
+                     : packed_matvec<NW, false, false>(G, kc, n, x, out, part, kmax, y, L.red);
       };
-      const bool q_given = PACKED && start_column<NW, RES>(G, G32, kc, n, L.q, L.w, part, kmax, L.red, glds, lds_n);
+      const bool q_given = PACKED && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
       NR_STAMP(8);  // start column
       const bool gv_rel = !dual;
       lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel);
@@ -2164,68 +1864,32 @@ module_profile_packed4_kernel(ProfileParams P) {
 }
 
 // Packed modules beyond the compile-time layout (runtime LDS layout, one
-// workgroup per CU): the 64 x 64 super-tile Gram at one wave per SIMD.
-#ifndef NR_BIG_G64
-#define NR_BIG_G64 1
-#endif
+// workgroup per CU): the 64 x 64 super-tile Gram at one wave per SIMD. (The
+// 128 x 128 LDS-staged workgroup tile measured 8% slower on C5 and was
+// removed, profiles/r04/ab7/.)
 __global__ void __launch_bounds__(NR_BS, 1)
 module_profile_big_kernel(ProfileParams P) {
   profile_body<NR_WAVES, true, 0, 0, false, true>(P);
 }
 
-// The same with the 128 x 128 workgroup-tile Gram (NR_BIG_G128).
-__global__ void __launch_bounds__(NR_BS, 1)
-module_profile_big128_kernel(ProfileParams P) {
-  profile_body<NR_WAVES, true, 0, 0, false, true, false, false, true>(P);
-}
-
-// The idle LDS vectors and partials of the large-module kernel hold a stage of
-// the 128 x 128 tile's operand slices (profile_body's overlay).
-bool big_g128_fits(const ProfileParams& P) {
-  const int kmax = P.kvec > 0 ? P.kvec : P.k_max;
-  return NR_BIG_G128 && NR_WAVES == 4 &&
-         6 * (int64_t)kmax + packed_part_doubles(NR_WAVES, kmax, P.m_max) >= (NR_G128_PF == 2 ? 2 : 1) * kG128Stage;
-}
-
 // The Gram-table launches of the packed class (every item fused, k <= S).
-#ifndef NR_TABLE_KERNEL
-#define NR_TABLE_KERNEL 1
-#endif
+// (An LDS prefix of the item's Gram and a CU-resident one-workgroup-per-CU
+// version measured equal and 1.8x slower: profiles/r04/ab4/, r04/resident/.)
 __global__ void __launch_bounds__(kTableWaves * 64, 3)
 module_profile_table_kernel(ProfileParams P) {
-  profile_body<kTableWaves, true, kPackedLayoutK, 0, true, false, NR_TABLE_LDS != 0>(P);
-}
-
-// The CU-resident Gram-table kernel: one kResWaves-wave workgroup per CU (two
-// waves per SIMD, 256 VGPRs), the packed Gram's leading units in LDS.
-__global__ void __launch_bounds__(kResWaves * 64, kResWaves / 4)
-module_profile_resident_kernel(ProfileParams P) {
-  profile_body<kResWaves, true, kPackedLayoutK, 0, true, false, true>(P);
+  profile_body<kTableWaves, true, kPackedLayoutK, 0, true>(P);
 }
 
 // The small class: Lanczos dimension <= kSmallDim (MB = KB = kSmallDim), NW
 // waves per item; three waves per SIMD (HIP's second launch bound is waves per
 // execution unit: the 168-VGPR budget of the packed kernel), as many items
-// per CU as the LDS holds.
-#ifndef NR_SMALL_OCC
-#define NR_SMALL_OCC 3
-#endif
-#ifndef NR_SMALL_FUSE
-#define NR_SMALL_FUSE 0  // tuning: 1 = the small class computes its items' network statistics (C2 measured
-                         // 1.6x slower: synchronous gathers in two-wave workgroups, spills; profiles/r04/)
-#endif
+// per CU as the LDS holds. (Computing the items' network statistics in the
+// same workgroups measured 1.6x slower on C2, profiles/r04/ab2/.)
+constexpr int kSmallOcc = 3;
 template <int NW>
-__global__ void __launch_bounds__(NW * 64, NR_SMALL_OCC)
+__global__ void __launch_bounds__(NW * 64, kSmallOcc)
 module_profile_small_kernel(ProfileParams P) {
-  profile_body<NW, true, kSmallDim, kSmallDim, false, false, false, NR_SMALL_FUSE != 0>(P);
-}
-
-bool small_fuse_enabled() { return NR_SMALL_FUSE != 0; }
-
-size_t small_fused_lds(int k_max) {
-  const size_t net = net_lds_bytes(kSmallWaves, k_max > kSmallDim ? k_max : kSmallDim);
-  const size_t own = profile_small_lds();
-  return net > own ? net : own;
+  profile_body<NW, true, kSmallDim, kSmallDim>(P);
 }
 
 // ---------------------------------------------------------------------------
@@ -2334,7 +1998,7 @@ __global__ void colsum_kernel(const double* __restrict__ X, int S, int64_t n, do
 // element, 32 x 32 tiles (net^T staged in LDS so both reads are coalesced).
 __global__ void __launch_bounds__(256)
 widen_pairs_kernel(const double2* __restrict__ in, const double* __restrict__ gram, double2* __restrict__ out,
-                   int64_t n, int symmetric, int packed) {
+                   int64_t n, int symmetric) {
   __shared__ double t[32][33];
   const int64_t r0 = (int64_t)blockIdx.x * 32, c0 = (int64_t)blockIdx.y * 32;
   const int i = threadIdx.x & 31;
@@ -2351,7 +2015,7 @@ widen_pairs_kernel(const double2* __restrict__ in, const double* __restrict__ gr
     const int64_t r = r0 + i, c = c0 + j;
     if (r < n && c < n) {
       const int64_t e = r + c * n;
-      const double2 p = in[packed ? tri_at(r, c, n) : e];  // packed input: symmetric matrices
+      const double2 p = in[e];
       out[2 * e] = p;
       out[2 * e + 1] = make_double2(gram[e], symmetric ? p.y : t[i][j]);   // net(c, r)
     }
@@ -2487,27 +2151,6 @@ size_t profile_table_lds() {
          sizeof(uint32_t) * kb;
 }
 
-size_t profile_resident_carve() {
-  constexpr int nw = kResWaves, kb = kPackedLayoutK, mb = kPackedLayoutK < 160 ? kPackedLayoutK : 160;
-  return sizeof(double) * (8 * nw + 6 * (size_t)kb + packed_part_doubles(nw, kb, mb) + 7 * (size_t)mb + 3) +
-         ((sizeof(uint32_t) * kb + 15) & ~(size_t)15);
-}
-
-int64_t profile_resident_gram_doubles() {
-  return (int64_t)((160 * 1024 - 64 - profile_resident_carve()) / sizeof(double)) / 32 * 32;
-}
-
-int64_t profile_table_gram_lds_doubles() {
-  if (!NR_TABLE_LDS) return 0;
-  // LDS is allocated per workgroup in 512-byte granules (static + dynamic):
-  // the three workgroups of a CU must still fit (a first sizing that ignored
-  // the granule left room for only two: profiles/r04/ab2)
-  const int per_cu = profile_table_per_cu();
-  const int64_t share = (int64_t)(160 * 1024 / per_cu) / 512 * 512 - 512;
-  const int64_t avail = share - (int64_t)profile_table_lds();
-  return avail > 0 ? avail / (int64_t)sizeof(double) / 32 * 32 : 0;
-}
-
 int profile_table_per_cu() {
   const int by_lds = (int)((160 * 1024) / profile_table_lds());
   const int by_waves = 12 / kTableWaves;
@@ -2523,7 +2166,7 @@ size_t profile_small_lds() {
 // items per CU: the LDS bound, at most 12 waves (the kernel's 168-VGPR budget)
 int profile_small_per_cu() {
   const int by_lds = (int)((160 * 1024) / profile_small_lds());
-  const int by_waves = 4 * NR_SMALL_OCC / kSmallWaves;
+  const int by_waves = 4 * kSmallOcc / kSmallWaves;
   return by_lds < by_waves ? by_lds : by_waves;
 }
 
@@ -2532,14 +2175,11 @@ hipError_t launch_net(const NetParams& P0, int64_t n_items, hipStream_t st) {
   P.n_items = n_items;
   if (n_items <= 0) return hipSuccess;
   const size_t lds = net_kernel_lds(P.k_max);
-  // the pairs' layout as a template argument where it is one of the two
-  // plain ones (packed triangle: symmetric only); the Gram table's stride at
-  // run time
+  // the pairs' layout as a template argument where it is the plain one; the
+  // Gram table's stride at run time
 #define NR_NET_LAUNCH(NW_, BIG_, GRID, BLOCK)                                                                \
   do {                                                                                                      \
-    if (P.symmetric && P.es == 0)                                                                           \
-      hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, true, 0>), GRID, BLOCK, lds, st, P);                 \
-    else if (P.symmetric && P.es == 1)                                                                      \
+    if (P.symmetric && P.es == 1)                                                                           \
       hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, true, 1>), GRID, BLOCK, lds, st, P);                 \
     else if (P.symmetric)                                                                                   \
       hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, true, -1>), GRID, BLOCK, lds, st, P);                \
@@ -2548,7 +2188,6 @@ hipError_t launch_net(const NetParams& P0, int64_t n_items, hipStream_t st) {
     else                                                                                                    \
       hipLaunchKernelGGL((module_net_kernel<NW_, BIG_, false, -1>), GRID, BLOCK, lds, st, P);               \
   } while (0)
-  if (!P.symmetric && P.es == 0) return hipErrorInvalidValue;  // the packed layout is for symmetric matrices
   if (net_kernel_big(P.k_max)) {
     if (!P.big_scratch || P.big_slots <= 0) return hipErrorInvalidValue;
     const unsigned g = (unsigned)(n_items < P.big_slots ? n_items : P.big_slots);
@@ -2570,28 +2209,19 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
     // the compile-time layout of modules of <= 320 nodes at three workgroups
     // per CU (measured fastest: profiles/r02/profile_variants.txt), else the
     // runtime layout
-    if (NR_TABLE_RESIDENT && P.fused == 1 && P.lds_gram_n > 0 && packed_bucket(P.k_max) == kPackedLayoutK)
-      hipLaunchKernelGGL(module_profile_resident_kernel, g, dim3(64 * kResWaves),
-                         profile_resident_carve() + sizeof(double) * (size_t)P.lds_gram_n, st, P);
-    else if (NR_TABLE_KERNEL && P.fused == 1 && packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3) {
-      ProfileParams Q = P;
-      Q.lds_gram_n = profile_table_gram_lds_doubles();
-      hipLaunchKernelGGL(module_profile_table_kernel, g, dim3(64 * kTableWaves),
-                         profile_table_lds() + sizeof(double) * (size_t)Q.lds_gram_n, st, Q);
-    }
+    if (P.fused == 1 && packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
+      hipLaunchKernelGGL(module_profile_table_kernel, g, dim3(64 * kTableWaves), profile_table_lds(), st, P);
     else if (packed_bucket(P.k_max) == kPackedLayoutK && wg_per_cu >= 3)
       hipLaunchKernelGGL((module_profile_packed4_kernel<kPackedLayoutK, 3>), g, b4, lds, st, P);
-    else if (NR_BIG_G64 && wg_per_cu == 1 && !P.fused && big_g128_fits(P))
-      hipLaunchKernelGGL(module_profile_big128_kernel, g, b4, lds, st, P);
-    else if (NR_BIG_G64 && wg_per_cu == 1 && !P.fused)
+    else if (wg_per_cu == 1 && !P.fused)
       hipLaunchKernelGGL(module_profile_big_kernel, g, b4, lds, st, P);
     else
       hipLaunchKernelGGL((module_profile_packed4_kernel<0, 2>), g, b4, lds, st, P);
     return hipGetLastError();
   }
   if (variant == 5) {
-    hipLaunchKernelGGL((module_profile_small_kernel<kSmallWaves>), g, dim3(64 * kSmallWaves),
-                       P.fused == 2 ? small_fused_lds(P.k_max) : profile_small_lds(), st, P);
+    hipLaunchKernelGGL((module_profile_small_kernel<kSmallWaves>), g, dim3(64 * kSmallWaves), profile_small_lds(),
+                       st, P);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(module_profile_kernel, g, b4, lds, st, P);
@@ -2616,24 +2246,9 @@ hipError_t launch_gram_full(const double* X, int64_t S, int64_t n, double* gram,
 }
 
 hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* out, int64_t n, int symmetric,
-                              int packed, hipStream_t st) {
+                              hipStream_t st) {
   const unsigned nb = (unsigned)((n + 31) / 32);
-  hipLaunchKernelGGL(widen_pairs_kernel, dim3(nb, nb), dim3(256), 0, st, in, gram, out, n, symmetric, packed);
-  return hipGetLastError();
-}
-
-// Full n x n pairs -> the packed lower triangle (symmetric matrices): column j
-// of the triangle is rows j..n-1 of column j, contiguous on both sides.
-__global__ void pack_pairs_kernel(const double2* __restrict__ in, double2* __restrict__ out, int64_t n) {
-  const int64_t j = blockIdx.y;
-  const int64_t base = j * n - j * (j - 1) / 2 - j;
-  for (int64_t i = j + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[base + i] = in[i + j * n];
-}
-
-hipError_t launch_pack_pairs(const double2* in, double2* out, int64_t n, hipStream_t st) {
-  const unsigned gx = (unsigned)std::min<int64_t>((n + 255) / 256, 16);
-  hipLaunchKernelGGL(pack_pairs_kernel, dim3(gx, (unsigned)n), dim3(256), 0, st, in, out, n);
+  hipLaunchKernelGGL(widen_pairs_kernel, dim3(nb, nb), dim3(256), 0, st, in, gram, out, n, symmetric);
   return hipGetLastError();
 }
 

@@ -71,6 +71,24 @@ def test_discovery_dataset_uploaded_once_for_three_test_datasets():
     N.IntermediateProperties(dxs, dc, dn, t_lists[0], ma, lay.modules)
     assert N.h2d_bytes() - before >= full
     c[0, 0] = old
+    # an edit between any sampling points (one node's row and
+    # column zeroed in the middle of the matrix) is seen too: every element is
+    # fingerprinted
+    mid = n // 2 + 7
+    saved_r, saved_c = c[mid, :].copy(), c[:, mid].copy()
+    c[mid, :] = 0.0
+    c[:, mid] = 0.0
+    before = N.h2d_bytes()
+    N.IntermediateProperties(dxs, dc, dn, t_lists[0], ma, lay.modules)
+    assert N.h2d_bytes() - before >= full
+    c[mid, :] = saved_r
+    c[:, mid] = saved_c
+    # one element changed by one ulp
+    c[mid + 1, 3] = np.nextafter(c[mid + 1, 3], 2.0)
+    before = N.h2d_bytes()
+    N.IntermediateProperties(dxs, dc, dn, t_lists[0], ma, lay.modules)
+    assert N.h2d_bytes() - before >= full
+    c[mid + 1, 3] = np.nextafter(c[mid + 1, 3], -2.0)
     # bitwise the results of fresh uploads
     for t, o in zip(t_lists, outs):
         N.ReleaseResident()
@@ -160,3 +178,67 @@ def test_broadcast_dataset_three_contexts_bitwise(n, s):
     finally:
         for e in engines:
             e.close()
+
+
+def test_cancel_after_run_does_not_stick_to_a_cleared_context():
+    """a context cancelled after its run returned (the progress
+    monitor cancels every context of a call) must not stop the next run once
+    its dataset is cleared for the pool (nr_clear_dataset)."""
+    from netrep_amd import _lib as L
+    lay, names, ma, x, c, nt = _dataset(n=800, s=40, seed=51, sizes=(60, 30))
+    eng = N.Engine(0)
+    try:
+        node_off, idx = S.csr_of(lay)
+        k = node_off[1:] - node_off[:-1]
+        dcv, dwd = np.zeros(int((k * (k - 1) // 2).sum())), np.zeros(int(k.sum()))
+
+        def load():
+            eng.set_dataset(c, nt, None)
+            eng.set_modules(len(k), np.arange(len(k), dtype=np.int32), node_off, idx, idx, dcv, dwd)
+            eng.set_null_pool(np.arange(len(names), dtype=np.int32))
+
+        load()
+        eng.run(0, 8, seed=3)
+        eng.cancel()                      # after the run: nothing left to stop
+        assert eng._lib.nr_clear_dataset(eng._h) == L.NR_OK
+        load()
+        out = eng.run(0, 8, seed=3)       # would raise NR_ERR_CANCELLED before the fix
+        assert out.shape[-1] == 8
+    finally:
+        eng.close()
+
+
+def test_pooled_context_host_threads_back_to_default():
+    """a pooled context returns to the process default host-thread
+    count, whatever nCores the call that used it passed."""
+    from netrep_amd import _lib as L
+    lib = L.load()
+    default = lib.nr_get_host_threads()
+    assert 1 <= default <= 16
+
+
+@pytest.mark.skipif(N.device_count() < 2, reason="needs two physical GPUs")
+def test_broadcast_across_two_physical_devices_bitwise():
+    """nr_broadcast_dataset between two physical GPUs
+    enables peer access (xGMI) and the copy runs bitwise like the source."""
+    from oracle import netrep_oracle as O
+    lay = S.make_layout(900, [120, 64, 30], 61)
+    x, c, nt = S.numpy_dataset(lay, 40, 62)
+    mi = O.ModuleIndex(lay.names, lay.labels, lay.names, lay.modules)
+    disc = O.intermediate_properties(O.scale(x), c, nt, mi.disc_idx(lay.names), with_data=True)
+    mods = mi.mods_present
+    node_off = np.concatenate([[0], np.cumsum([mi.test_idx[m].size for m in mods])])
+    with N.Engine(0) as a, N.Engine(1) as b:
+        a.set_dataset(c, nt, O.scale(x))
+        a.broadcast_dataset_to([b])
+        outs = []
+        for e in (a, b):
+            e.set_modules(len(mi.modules), [mi.modules.index(m) for m in mods], node_off,
+                          np.concatenate([mi.test_idx[m] for m in mods]),
+                          np.concatenate([mi.null_pos[m] for m in mods]),
+                          np.concatenate([disc["corr"][m] for m in mods]),
+                          np.concatenate([disc["degree"][m] for m in mods]),
+                          np.concatenate([disc["contribution"][m] for m in mods]))
+            e.set_null_pool(mi.null_idx)
+            outs.append(e.run(0, 32, seed=9))
+        _same_arr(outs[0], outs[1])
