@@ -277,21 +277,13 @@ def table_bytes(sizes):
     return (4 * k + 8 * k * (k - 1) / 2 + 32 * k * (k + 1) / 2 + 8 * k).sum()
 
 
-# Random 16-byte gathers over a 6.4 GB matrix on MI355X (tools/probes/gather_probe.hip,
-# profiles/r02/gather_probe.txt): the line rate the network kernel is bound by.
-GATHER_CEILING_GREADS = 50.0
-# the same probe over the C5 footprint (40,000 nodes, 25.6 GB): profiles/r03/c2c5/gather_probe_40k.txt
-GATHER_CEILING_C5_GREADS = 48.4
-
-
-def gather_ceiling(sizes, perms, seconds):
-    """The network kernel against the measured random-gather ceiling: one
-    16-byte {corr, net} read per unordered pair of every module."""
-    k = np.asarray(sizes, dtype=np.int64)
-    reads = float((k * (k - 1) // 2).sum()) * perms
-    g = reads / seconds / 1e9
-    return {"achieved": g, "peak": GATHER_CEILING_GREADS, "unit": "G 16-byte reads/s", "frac": g / GATHER_CEILING_GREADS,
-            "source": "profiles/r02/gather_probe.txt"}
+# The network statistics' launches (timer 0): the column sweep (sweep.hip) --
+# each test column streamed into LDS once per batch, every occurrence of the
+# column reading its rows there -- so no random-gather ceiling applies; the
+# roofline is SURVEY.md 8d's network bytes against HBM peak.
+NET_KERNEL = "network_sweep"
+NET_UNITS = ("achieved = SURVEY.md 8d network bytes 4k + 8k(k-1)/2 + 8k^2 per module-permutation x the "
+             "launch's items / HIP-event time of the sweep's five kernels (sweep.hip)")
 
 
 def time_steps(eng, world, rank, steps, warmup, perms_per_step, seed, base_warm):
@@ -509,7 +501,7 @@ def run_c5(args, world, rank, local):
         "compute_perms_per_sec": P / compute_s,
         "pipelined_s_per_dataset": elapsed / (3 * K),
         "call_s": call_s,
-        "kernels": {"module_net_kernel": {"avg_ms": ms0 / max(l0, 1), "launches": l0},
+        "kernels": {NET_KERNEL: {"avg_ms": ms0 / max(l0, 1), "launches": l0},
                     "module_profile_kernel": {"avg_ms": ms1 / max(l1, 1), "launches": l1,
                                               "achieved": prof_f * P / (ms1 * 1e-3) / 1e12 if ms1 > 0 else None,
                                               "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s"}},
@@ -518,11 +510,6 @@ def run_c5(args, world, rank, local):
     mk = line["kernels"]["module_profile_kernel"]
     if mk["achieved"] is not None:
         mk["frac"] = mk["achieved"] / mk["peak"]
-    nk = line["kernels"]["module_net_kernel"]
-    if ms0 > 0:
-        nk["gather_ceiling"] = gather_ceiling(sizes, P / max(l0, 1), ms0 / max(l0, 1) / 1e3)
-        nk["gather_ceiling"]["peak_c5_footprint"] = GATHER_CEILING_C5_GREADS
-        nk["gather_ceiling"]["frac_c5_footprint"] = nk["gather_ceiling"]["achieved"] / GATHER_CEILING_C5_GREADS
     # the dominant kernel (the summary-profile launches of one batch: the
     # large modules' Gram executes on the matrix cores)
     b_launch = int(round(P / max(l1, 1)))
@@ -619,13 +606,12 @@ def main():
                 "value": tot2 / el2, "unit": "permutations/sec", "steps": args.secondary_steps,
                 "perms_per_step": P2, "launch_batch": B2, "ms_per_step": el2 / args.secondary_steps * 1e3,
                 "finite_fraction": fin2,
-                "roofline": {"kernel": "module_net_kernel", "bound": "hbm", "avg_ms": ms2 / max(l2, 1),
+                "roofline": {"kernel": NET_KERNEL, "bound": "hbm", "avg_ms": ms2 / max(l2, 1),
                              "achieved": net_b * B2 / t2 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": net_b * B2 / t2 / 1e9 / HBM_PEAK_GBS,
-                             "algorithmic_bytes": round(net_b * B2)},
-                "gather_ceiling": gather_ceiling(lay.module_sizes, B2, t2),
+                             "algorithmic_bytes": round(net_b * B2), "units_note": NET_UNITS},
             }
-            secondary["roofline"].update(traffic_fields("C4", B2, "module_net_kernel", ms2 / max(l2, 1)))
+            secondary["roofline"].update(traffic_fields("C4", B2, NET_KERNEL, ms2 / max(l2, 1)))
         eng2.close()
 
     if rank == 0:
@@ -635,11 +621,10 @@ def main():
         fused = meta["with_data"] and l0 == 0   # network statistics computed inside the profile kernel
         if l0 > 0:
             t0 = ms0 / l0 / 1e3
-            kernels["module_net_kernel"] = {
+            kernels[NET_KERNEL] = {
                 "bound": "hbm", "avg_ms": ms0 / l0, "launches": l0,
                 "achieved": net_b * B / t0 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "algorithmic_bytes": round(net_b * B),
-                "gather_ceiling": gather_ceiling(lay.module_sizes, B, t0)}
+                "algorithmic_bytes": round(net_b * B), "units_note": NET_UNITS}
         table = meta["with_data"] and eng.gram_table()
         if table:
             # Gram table: every statistic of a module-permutation in this one
@@ -666,7 +651,6 @@ def main():
                 "table_gather_bytes": {"achieved": tab_b * B / t1 / 1e9, "unit": "GB/s",
                                        "note": "32-byte table element per pair and diagonal entry + indices + "
                                                "discovery vectors, the bytes this kernel's gathers need"},
-                "gather_ceiling": gather_ceiling(lay.module_sizes, B, t1),
                 "table_build_ms": eng.gram_table_ms(),
                 "table_build_note": "one-off per test dataset, in the first (warm-up) run: X^T X on the "
                                     "matrix cores + the widened {corr, net, gram, net^T} layout; outside "
@@ -694,7 +678,7 @@ def main():
         roofline["traffic_unit"] = ("L2-miss bytes/launch incl. Infinity Cache hits (rocprofv3 FETCH_SIZE x2 + "
                                     "WRITE_SIZE; traffic_range = [raw, x2]; profiles/pmc_traffic.json)")
         if table and dom_name == "module_profile_kernel":
-            for key in ("gram_table", "f_units", "gather_ceiling", "table_build_ms"):
+            for key in ("gram_table", "f_units", "table_build_ms"):
                 roofline[key] = dom[key]
         roofline["executed"] = measured_mfma(args.config, B, dom_name, dom["avg_ms"], bool(table))
         cpu = None

@@ -69,6 +69,7 @@ struct nr_ctx {
   int64_t null_gen = -1;                // data_gen the null pool was validated against
   int symmetric = 0;
   int corr_finite = 0, net_finite = 0;  // CheckFinite of the resident matrices
+  int disc_cv_finite = 0;               // the present modules' discovery CorrVector is all finite
 
   // modules
   int32_t n_rows = 0, n_present = 0, k_max = 0;
@@ -86,6 +87,8 @@ struct nr_ctx {
   double* d_cv_shift = nullptr;
   int32_t* d_mod_order = nullptr;
   std::vector<int32_t> order_k_h;  // module sizes in d_mod_order's order (descending)
+  int32_t* d_node_mod = nullptr;   // [n_node_total] module of each CSR node (the column sweep)
+  int32_t* d_node_order = nullptr; // [n_node_total] CSR nodes by module size, descending (the column sweep)
 
   // null pool
   int32_t* d_null_idx = nullptr;
@@ -124,6 +127,18 @@ struct nr_ctx {
   double* d_obs = nullptr;
   size_t obs_cap = 0;
   bool obs_pending = false;  // cleared by every change of dataset, modules or null pool
+
+  // the column sweep's per-batch work buffers (sweep.hip), one set per lane
+  struct SweepBuf {
+    int32_t *col = nullptr, *rank = nullptr, *count = nullptr, *col_off = nullptr, *bnd = nullptr;
+    uint32_t *sorted = nullptr, *bndh = nullptr;
+    uint4* meta = nullptr;
+    double *ys = nullptr, *rec = nullptr, *dabs = nullptr;
+    double* zs = nullptr;  // [4] zeros + [128] sink (sweep.hip: lanes with nothing to load / store)
+    double2* shiftv = nullptr;
+    size_t occ_cap = 0, col_cap = 0, item_cap = 0;
+    int32_t chunk_cap = 0;
+  } sweep[2];
 
   std::atomic<int64_t> done{0}, total{0};
   std::atomic<bool> cancel{false};
@@ -592,6 +607,112 @@ int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std
   return NR_OK;
 }
 
+// The column sweep for one batch (sweep.hip) on the lane's buffers.
+// Sub-batches of at most kSweepMaxOcc (permutation, node) occurrences (int32
+// occurrence ids, bounded buffers); an item's statistics do not depend on
+// the batch it runs in, so neither do the results.
+constexpr int64_t kSweepMaxOcc = (int64_t)64 << 20;
+
+int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const Lane& ln);
+
+int launch_sweep_batch(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const Lane& ln) {
+  const int64_t per = std::max<int64_t>(1, kSweepMaxOcc / std::max<int64_t>(ctx->n_node_total, 1));
+  for (int64_t p0 = 0; p0 < n_perm; p0 += per) {
+    const int64_t np_sub = std::min(per, n_perm - p0);
+    nr::NetParams q = np;
+    q.src.perm_base = np.src.perm_base + p0;
+    if (q.src.mode == nr::NR_IDX_TABLE) q.src.pi = np.src.pi + p0 * (int64_t)np.src.n_null;
+    q.out = np.out + p0 * (int64_t)np.n_rows * np.n_stat;
+    if (int rc = launch_sweep_sub(ctx, q, np_sub, ln)) return rc;
+  }
+  return NR_OK;
+}
+
+int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const Lane& ln) {
+  nr_ctx::SweepBuf& b = ctx->sweep[ln.id];
+  const size_t n_occ = (size_t)(n_perm * ctx->n_node_total);
+  const size_t n_items = (size_t)(n_perm * ctx->n_present);
+  nr::SweepParams P{};
+  P.chunk_rows = nr::sweep_chunk_rows(ctx->n_nodes, np.disc_cv ? 16 : 8);
+  P.n_chunks = (int32_t)((ctx->n_nodes + P.chunk_rows - 1) / P.chunk_rows);
+  auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t per) -> int {
+    (void)cap;
+    dfree(ptr);
+    NR_HIP(ctx, hipMalloc((void**)&ptr, std::max<size_t>(need, 1) * per));
+    return NR_OK;
+  };
+  int rc;
+  if (n_occ > b.occ_cap || P.n_chunks > b.chunk_cap) {
+    size_t c = 0;
+    if ((rc = grow(b.col, c, n_occ, 4)) || (rc = grow(b.rank, c, n_occ, 4)) ||
+        (rc = grow(b.sorted, c, n_occ, 4)) || (rc = grow(b.meta, c, n_occ, sizeof(uint4))) ||
+        (rc = grow(b.shiftv, c, n_occ, 16)) || (rc = grow(b.bndh, c, n_occ, 4 * (size_t)P.n_chunks)) ||
+        (rc = grow(b.rec, c, n_occ, 8 * nr::kSweepRec * (size_t)P.n_chunks)))
+      return rc;
+    b.occ_cap = n_occ;
+    b.chunk_cap = P.n_chunks;
+  }
+  if (!b.zs) {
+    NR_HIP(ctx, hipMalloc((void**)&b.zs, (4 + 128) * sizeof(double)));
+    NR_HIP(ctx, hipMemsetAsync(b.zs, 0, 4 * sizeof(double), ln.st));
+  }
+  const size_t n_cols = (size_t)ctx->n_nodes + 1;
+  if (n_cols > b.col_cap) {
+    size_t c = 0;
+    if ((rc = grow(b.count, c, n_cols, 4)) || (rc = grow(b.col_off, c, n_cols, 4)) || (rc = grow(b.dabs, c, n_cols, 8)))
+      return rc;
+    b.col_cap = n_cols;
+  }
+  const size_t item_need = n_items * (size_t)(nr::kSweepMaxChunks + 1);
+  if (item_need > b.item_cap) {
+    size_t c = 0;
+    if ((rc = grow(b.bnd, c, item_need, 4)) || (rc = grow(b.ys, c, item_need, 8))) return rc;
+    b.item_cap = item_need;
+  }
+  P.pairs = np.pairs;
+  P.n_nodes = ctx->n_nodes;
+  P.es = np.es;
+  P.src = np.src;
+  P.n_node_total = ctx->n_node_total;
+  P.n_present = ctx->n_present;
+  P.node_off = ctx->d_node_off;
+  P.node_mod = ctx->d_node_mod;
+  P.node_order = ctx->d_node_order;
+  P.cv_off = ctx->d_cv_off;
+  P.disc_cv = np.disc_cv;
+  P.n_cv = ctx->n_cv_total;
+  P.finite = ctx->corr_finite && ctx->disc_cv_finite;
+  P.disc_wd = np.disc_wd;
+  P.cv_shift = np.cv_shift;
+  P.n_perm = (int32_t)n_perm;
+  P.k_max = ctx->k_max;
+  P.n_occ = (int64_t)n_occ;
+  P.col = b.col;
+  P.sorted = b.sorted;
+  P.rank = b.rank;
+  P.count = b.count;
+  P.col_off = b.col_off;
+  P.dabs = b.dabs;
+  P.zero = b.zs;
+  P.sink = b.zs + 4;
+  P.bnd = b.bnd;
+  P.ys = b.ys;
+  P.meta = b.meta;
+  P.bndh = b.bndh;
+  P.shiftv = np.disc_cv ? b.shiftv : nullptr;
+  P.rec = b.rec;
+  P.row_of = np.row_of;
+  P.n_rows = np.n_rows;
+  P.n_stat = np.n_stat;
+  P.slot_avg_weight = np.slot_avg_weight;
+  P.slot_cor_cor = np.slot_cor_cor;
+  P.slot_cor_degree = np.slot_cor_degree;
+  P.slot_avg_cor = np.slot_avg_cor;
+  P.out = np.out;
+  NR_HIP(ctx, nr::launch_sweep(P, ln.st));
+  return NR_OK;
+}
+
 // Launch the statistics kernels for n_perm permutations (or the observed /
 // direct sets when src.mode == NR_IDX_DIRECT, n_perm == 1) into d_out.
 int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double* d_out, const Lane& ln) {
@@ -635,6 +756,16 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
   // phase fused into the profile items without the table at +0.7%, within
   // run-to-run noise, and on a concurrent stream at -11%.)
   const bool table = data && ctx->pairs_es == 2;
+  // Without the Gram table the network statistics of every present module
+  // come from the column sweep (sweep.hip: each test column streamed into LDS
+  // once per batch) where the shapes allow it (n < 65,536, modules of at most
+  // 4,096 nodes); the item-major gather kernel otherwise. The choice depends
+  // on the shapes only.
+  if (!table && nr::sweep_supported(ctx->n_nodes, ctx->k_max)) {
+    if (ln.timed) timer_begin(ctx, 0, ln.st);
+    if ((rc = launch_sweep_batch(ctx, np, n_perm, ln))) return rc;
+    if (ln.timed) timer_end(ctx, 0, n_items, ln.st);
+  }
   auto nets = [&](int n_mod) -> int {
     if (n_mod <= 0) return NR_OK;
     std::vector<int32_t> ks(ctx->order_k_h.begin(), ctx->order_k_h.begin() + n_mod);
@@ -643,7 +774,7 @@ int launch_batch(nr_ctx* ctx, const nr::IndexSource& src, int64_t n_perm, double
     if (ln.timed) timer_end(ctx, 0, (int64_t)n_mod * n_perm, ln.st);
     return NR_OK;
   };
-  if (!table && (rc = nets(ctx->n_present))) return rc;
+  if (!table && !nr::sweep_supported(ctx->n_nodes, ctx->k_max) && (rc = nets(ctx->n_present))) return rc;
 
   if (data) {
     nr::ProfileParams pp{};
@@ -1013,6 +1144,23 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   dfree(ctx->d_disc_nc);
   dfree(ctx->d_cv_shift);
   dfree(ctx->d_mod_order);
+  dfree(ctx->d_node_mod);
+  dfree(ctx->d_node_order);
+  for (auto& b : ctx->sweep) {
+    dfree(b.col);
+    dfree(b.rank);
+    dfree(b.count);
+    dfree(b.col_off);
+    dfree(b.bnd);
+    dfree(b.sorted);
+    dfree(b.meta);
+    dfree(b.bndh);
+    dfree(b.ys);
+    dfree(b.shiftv);
+    dfree(b.dabs);
+    dfree(b.zs);
+    dfree(b.rec);
+  }
   dfree(ctx->d_null_idx);
   dfree(ctx->d_out);
   dfree(ctx->d_pi);
@@ -1629,6 +1777,12 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   ctx->k_max = kmax;
   ctx->n_node_total = ctx->node_off_h.back();
   ctx->n_cv_total = ctx->cv_off_h.back();
+  ctx->disc_cv_finite = 1;
+  for (int64_t v = 0; v < ctx->n_cv_total; ++v)
+    if (!std::isfinite(disc_corr[v])) {
+      ctx->disc_cv_finite = 0;
+      break;
+    }
   for (int64_t i = 0; i < ctx->n_node_total; ++i)
     if (test_idx[i] < 0 || test_idx[i] >= ctx->n_nodes)
       return fail(ctx, NR_ERR_INVALID, "test_idx outside the resident dataset (call nr_set_dataset first)");
@@ -1655,6 +1809,18 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   if ((rc = upload(ctx, ctx->d_disc_nc, disc_contrib, disc_contrib ? (size_t)ctx->n_node_total : 0))) return rc;
   if ((rc = upload(ctx, ctx->d_cv_shift, shift.data(), shift.size()))) return rc;
   if ((rc = upload(ctx, ctx->d_mod_order, order.data(), order.size()))) return rc;
+  {
+    std::vector<int32_t> node_mod((size_t)ctx->n_node_total);
+    for (int m = 0; m < n_present; ++m)
+      for (int64_t i = node_off[m]; i < node_off[m + 1]; ++i) node_mod[(size_t)i] = m;
+    std::vector<int32_t> node_order;
+    node_order.reserve((size_t)ctx->n_node_total);
+    for (int i = 0; i < n_present; ++i)
+      for (int64_t v = node_off[order[i]]; v < node_off[order[i] + 1]; ++v) node_order.push_back((int32_t)v);
+    if ((rc = upload(ctx, ctx->d_node_mod, node_mod.data(), node_mod.size()))) return rc;
+    if ((rc = upload(ctx, ctx->d_node_order, node_order.data(), node_order.size()))) return rc;
+    NR_HIP(ctx, hipStreamSynchronize(ctx->stream));  // node_mod, node_order are locals
+  }
   ctx->order_k_h.resize(n_present);
   for (int i = 0; i < n_present; ++i) ctx->order_k_h[i] = (int32_t)(node_off[order[i] + 1] - node_off[order[i]]);
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));

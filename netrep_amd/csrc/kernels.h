@@ -107,6 +107,61 @@ struct ProfileParams {
   NetParams net;
 };
 
+// The column sweep (sweep.hip): network statistics of a batch organised by
+// test column (each column chunk streamed into LDS once, every occurrence of
+// the column reads its rows there) instead of one random gather per pair.
+constexpr int kSweepWaves = 16;                   // waves per (column, chunk) workgroup: one per CU
+constexpr int kSweepLanes = 16;                   // lanes per occurrence
+constexpr int kSweepMaxChunks = 16;               // chunks per column (n <= 65,535)
+constexpr int kSweepMaxK = 4096;                  // module nodes (LDS of the per-item kernels)
+constexpr int64_t kSweepChunkBytes = 160000;      // LDS per (column, chunk) workgroup
+constexpr int kSweepRec = 12;                     // doubles per (occurrence, chunk) record
+struct SweepParams {
+  const double2* pairs;        // {corr, net} (es = 1) or the Gram table (es = 2), column-major n x n
+  int64_t n_nodes;
+  int32_t es;
+  IndexSource src;
+  int64_t n_node_total;        // module nodes of the present modules (CSR)
+  int32_t n_present;
+  const int64_t* node_off;     // [n_present + 1]
+  const int32_t* node_mod;     // [n_node_total] module of each CSR node
+  const int32_t* node_order;   // [n_node_total] CSR nodes by module size (descending)
+  const int64_t* cv_off;       // [n_present + 1] CorrVector offsets
+  const double* disc_cv;       // discovery CorrVector (NULL: no CorrVector statistics)
+  int64_t n_cv;                // its length
+  int32_t finite;              // 1: the test correlations and disc_cv are all finite (no complete-case tests)
+  const double* disc_wd;       // discovery weighted degree
+  const double* cv_shift;      // [n_present] one-pass shift of the discovery values
+  int32_t n_perm;              // permutations of this batch
+  int32_t k_max;
+  int64_t n_occ;               // n_perm x n_node_total occurrences
+  int64_t chunk_rows;          // rows per column chunk
+  int32_t n_chunks;
+  // per batch work buffers
+  int32_t* col;                // [n_occ] test column of each (permutation, node)
+  uint32_t* sorted;            // [n_occ] per item: (column << 16 | position), sorted by column
+  int32_t* rank;               // [n_occ] sorted rank of each position
+  int32_t* count;              // [n_nodes] occurrences per column (then the scatter cursor)
+  int32_t* col_off;            // [n_nodes + 1]
+  const double* zero;          // >= 32 zero bytes: the address of a lane with nothing to load
+  double* sink;                // [128] the address of a lane with nothing to store
+  double* dabs;                // [n_nodes] |diagonal| of each column with occurrences (written by the sweep)
+  int32_t* bnd;                // [items x (n_chunks + 1)] first sorted entry of each chunk
+  double* ys;                  // [items] CorrVector shift of the test side
+  uint4* meta;                 // [n_occ] by column slot: item base, jj | rank << 16, CorrVector base, b1 | k << 16
+  uint32_t* bndh;              // [n_chunks x n_occ] by slot (more than two chunks): e0 | e1 << 16 of the chunk
+  double2* shiftv;             // [n_occ] by slot: CorrVector shifts {module, item} (CorrVector only)
+  double* rec;                 // [n_occ x n_chunks x kSweepRec] one record per (occurrence, chunk)
+  const int32_t* row_of;
+  int32_t n_rows, n_stat;
+  int32_t slot_avg_weight, slot_cor_cor, slot_cor_degree, slot_avg_cor;
+  double* out;
+};
+// rows per chunk for LDS elements of elem_bytes (16: {corr, net}; 8: net only)
+int64_t sweep_chunk_rows(int64_t n_nodes, int elem_bytes);
+bool sweep_supported(int64_t n_nodes, int k_max);
+hipError_t launch_sweep(const SweepParams& P, hipStream_t st);
+
 size_t net_kernel_lds(int k_max);
 bool net_kernel_big(int k_max);        // per-node arrays in global scratch
 size_t net_big_slot_bytes(int k_max);  // global scratch per workgroup in that mode

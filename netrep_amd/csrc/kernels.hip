@@ -65,24 +65,7 @@ namespace nr {
 // Bitwise equal to the two-accumulator loop in the cancellation regime
 // (tools check: oracle/netrep_ref.cpp vs the kernel, tests/test_gpu_configs.py).
 // ---------------------------------------------------------------------------
-constexpr int WD_FX_BITS = 16;        // fixed-point sub-units per grid unit
-constexpr int WD_NO_GRID = -100000;   // exponent sentinel: no cancellation model
-
-// Exponent of the grid unit g = 2^e of the accumulator holding d: the ulp of
-// d's binade, or of the next binade when d sits within 2^-20 below it (the
-// first addition then carries the accumulator across).
-__device__ __forceinline__ int wd_grid_exp(double d) {
-  if (!(d >= 2.2250738585072014e-308) || !isfinite(d)) return WD_NO_GRID;
-  const int e = ilogb(d);
-  const double top = ldexp(1.0, e + 1);
-  return (top - d <= ldexp(d, -20) ? e + 1 : e) - 52;
-}
-
-__device__ __forceinline__ unsigned long long wd_fx(double a, int ge, int extra) {
-  double v = ldexp(a, extra - ge);
-  v = v < 2.305843009213694e18 ? v : 2.305843009213694e18;  // 2^61: overflow is caught by the range check
-  return (unsigned long long)llrint(v);
-}
+// (WD_FX_BITS, WD_NO_GRID, wd_grid_exp, wd_fx: device_common.h)
 
 struct NetLds {
   double* red;                       // 8 * NW

@@ -1,0 +1,58 @@
+"""Round 5: rocprof evidence for the north star's Scale,
+CheckFinite and NetProps subsystems at the metric's size (20,000 genes x 500
+samples, the 50 C3 modules): each reference-interface call once, then again
+(the second NetProps / IntermediateProperties reuse the resident dataset).
+Run under `rocprofv3 --kernel-trace --stats` for the per-kernel durations.
+Prints one JSON line with the wall times and the algorithmic bytes of the
+device passes (Scale: read + write S x N doubles; CheckFinite: read n^2; the
+upload's symmetry/finite pass: read both n x n matrices)."""
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import netrep_amd as N  # noqa: E402
+from netrep_amd import synthetic as S  # noqa: E402
+from netrep_amd.api import RMatrix  # noqa: E402
+
+
+def main():
+    n, s = 20000, 500
+    sizes = np.round(np.linspace(30, 300, 50)).astype(int)
+    lay = S.make_layout(n, sizes, 11)
+    xt, corr, net = S.torch_dataset(lay, s, 12)
+    x = np.asfortranarray(xt.cpu().numpy().T)       # S x N column-major = the (N, S) row-major buffer
+    c = np.asfortranarray(corr.cpu().numpy())
+    nt = np.asfortranarray(net.cpu().numpy())
+    del xt, corr, net
+    torch.cuda.empty_cache()
+    names = lay.names
+    ma = dict(zip(names, lay.labels))
+    out = {"n": n, "s": s, "modules": len(lay.modules)}
+    t = time.time()
+    xs = N.Scale(RMatrix(x, None, names))
+    out["scale_s"] = time.time() - t
+    t = time.time()
+    N.CheckFinite(RMatrix(c, names, names))
+    out["checkfinite_s"] = time.time() - t
+    for rep in range(2):
+        t = time.time()
+        r = N.NetProps(RMatrix(x, None, names), RMatrix(nt, names, names), ma, lay.modules)
+        out[f"netprops_{rep}_s"] = time.time() - t
+    for rep in range(2):
+        t = time.time()
+        d = N.IntermediateProperties(xs, RMatrix(c, names, names), RMatrix(nt, names, names), names, ma,
+                                     lay.modules)
+        out[f"intermediate_{rep}_s"] = time.time() - t
+    out["coherence_mod1"] = float(r["1"]["coherence"])
+    out["n_contrib"] = int(sum(len(v) for v in d["contribution"].values()))
+    out["bytes"] = {"scale_kernel": 2 * 8 * n * s, "finite_kernel": 8 * n * n, "symmetry_kernel": 2 * 16 * n * n}
+    N.ReleaseResident()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
