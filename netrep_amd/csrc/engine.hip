@@ -87,8 +87,6 @@ struct nr_ctx {
   double* d_cv_shift = nullptr;
   int32_t* d_mod_order = nullptr;
   std::vector<int32_t> order_k_h;  // module sizes in d_mod_order's order (descending)
-  int32_t* d_node_mod = nullptr;   // [n_node_total] module of each CSR node (the column sweep)
-  int32_t* d_node_order = nullptr; // [n_node_total] CSR nodes by module size, descending (the column sweep)
 
   // null pool
   int32_t* d_null_idx = nullptr;
@@ -130,13 +128,12 @@ struct nr_ctx {
 
   // the column sweep's per-batch work buffers (sweep.hip), one set per lane
   struct SweepBuf {
-    int32_t *col = nullptr, *rank = nullptr, *count = nullptr, *col_off = nullptr, *bnd = nullptr;
+    int32_t *col = nullptr, *rank = nullptr, *lrank = nullptr, *count = nullptr, *col_off = nullptr;
     uint32_t *sorted = nullptr, *bndh = nullptr;
     uint4* meta = nullptr;
-    double *ys = nullptr, *rec = nullptr, *dabs = nullptr;
+    double *rec = nullptr, *dabs = nullptr;
     double* zs = nullptr;  // [4] zeros + [128] sink (sweep.hip: lanes with nothing to load / store)
-    double2* shiftv = nullptr;
-    size_t occ_cap = 0, col_cap = 0, item_cap = 0;
+    size_t occ_cap = 0, col_cap = 0;
     int32_t chunk_cap = 0;
   } sweep[2];
 
@@ -631,7 +628,6 @@ int launch_sweep_batch(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, con
 int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const Lane& ln) {
   nr_ctx::SweepBuf& b = ctx->sweep[ln.id];
   const size_t n_occ = (size_t)(n_perm * ctx->n_node_total);
-  const size_t n_items = (size_t)(n_perm * ctx->n_present);
   nr::SweepParams P{};
   P.chunk_rows = nr::sweep_chunk_rows(ctx->n_nodes, np.disc_cv ? 16 : 8);
   P.n_chunks = (int32_t)((ctx->n_nodes + P.chunk_rows - 1) / P.chunk_rows);
@@ -645,8 +641,9 @@ int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const
   if (n_occ > b.occ_cap || P.n_chunks > b.chunk_cap) {
     size_t c = 0;
     if ((rc = grow(b.col, c, n_occ, 4)) || (rc = grow(b.rank, c, n_occ, 4)) ||
-        (rc = grow(b.sorted, c, n_occ, 4)) || (rc = grow(b.meta, c, n_occ, sizeof(uint4))) ||
-        (rc = grow(b.shiftv, c, n_occ, 16)) || (rc = grow(b.bndh, c, n_occ, 4 * (size_t)P.n_chunks)) ||
+        (rc = grow(b.sorted, c, n_occ, 4)) || (rc = grow(b.lrank, c, n_occ, 4)) ||
+        (rc = grow(b.meta, c, n_occ, 2 * sizeof(uint4))) ||
+        (rc = grow(b.bndh, c, P.n_chunks > 2 ? n_occ : 0, 4 * (size_t)P.n_chunks)) ||
         (rc = grow(b.rec, c, n_occ, 8 * nr::kSweepRec * (size_t)P.n_chunks)))
       return rc;
     b.occ_cap = n_occ;
@@ -663,12 +660,6 @@ int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const
       return rc;
     b.col_cap = n_cols;
   }
-  const size_t item_need = n_items * (size_t)(nr::kSweepMaxChunks + 1);
-  if (item_need > b.item_cap) {
-    size_t c = 0;
-    if ((rc = grow(b.bnd, c, item_need, 4)) || (rc = grow(b.ys, c, item_need, 8))) return rc;
-    b.item_cap = item_need;
-  }
   P.pairs = np.pairs;
   P.n_nodes = ctx->n_nodes;
   P.es = np.es;
@@ -676,8 +667,7 @@ int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const
   P.n_node_total = ctx->n_node_total;
   P.n_present = ctx->n_present;
   P.node_off = ctx->d_node_off;
-  P.node_mod = ctx->d_node_mod;
-  P.node_order = ctx->d_node_order;
+  P.mod_order = ctx->d_mod_order;
   P.cv_off = ctx->d_cv_off;
   P.disc_cv = np.disc_cv;
   P.n_cv = ctx->n_cv_total;
@@ -695,11 +685,9 @@ int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const
   P.dabs = b.dabs;
   P.zero = b.zs;
   P.sink = b.zs + 4;
-  P.bnd = b.bnd;
-  P.ys = b.ys;
   P.meta = b.meta;
   P.bndh = b.bndh;
-  P.shiftv = np.disc_cv ? b.shiftv : nullptr;
+  P.lrank = b.lrank;
   P.rec = b.rec;
   P.row_of = np.row_of;
   P.n_rows = np.n_rows;
@@ -1144,19 +1132,15 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   dfree(ctx->d_disc_nc);
   dfree(ctx->d_cv_shift);
   dfree(ctx->d_mod_order);
-  dfree(ctx->d_node_mod);
-  dfree(ctx->d_node_order);
   for (auto& b : ctx->sweep) {
     dfree(b.col);
     dfree(b.rank);
     dfree(b.count);
     dfree(b.col_off);
-    dfree(b.bnd);
     dfree(b.sorted);
     dfree(b.meta);
     dfree(b.bndh);
-    dfree(b.ys);
-    dfree(b.shiftv);
+    dfree(b.lrank);
     dfree(b.dabs);
     dfree(b.zs);
     dfree(b.rec);
@@ -1809,18 +1793,6 @@ int nr_set_modules(nr_ctx* ctx, int32_t n_rows, int32_t n_present, const int32_t
   if ((rc = upload(ctx, ctx->d_disc_nc, disc_contrib, disc_contrib ? (size_t)ctx->n_node_total : 0))) return rc;
   if ((rc = upload(ctx, ctx->d_cv_shift, shift.data(), shift.size()))) return rc;
   if ((rc = upload(ctx, ctx->d_mod_order, order.data(), order.size()))) return rc;
-  {
-    std::vector<int32_t> node_mod((size_t)ctx->n_node_total);
-    for (int m = 0; m < n_present; ++m)
-      for (int64_t i = node_off[m]; i < node_off[m + 1]; ++i) node_mod[(size_t)i] = m;
-    std::vector<int32_t> node_order;
-    node_order.reserve((size_t)ctx->n_node_total);
-    for (int i = 0; i < n_present; ++i)
-      for (int64_t v = node_off[order[i]]; v < node_off[order[i] + 1]; ++v) node_order.push_back((int32_t)v);
-    if ((rc = upload(ctx, ctx->d_node_mod, node_mod.data(), node_mod.size()))) return rc;
-    if ((rc = upload(ctx, ctx->d_node_order, node_order.data(), node_order.size()))) return rc;
-    NR_HIP(ctx, hipStreamSynchronize(ctx->stream));  // node_mod, node_order are locals
-  }
   ctx->order_k_h.resize(n_present);
   for (int i = 0; i < n_present; ++i) ctx->order_k_h[i] = (int32_t)(node_off[order[i] + 1] - node_off[order[i]]);
   NR_HIP(ctx, hipStreamSynchronize(ctx->stream));

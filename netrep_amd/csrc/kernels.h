@@ -124,8 +124,7 @@ struct SweepParams {
   int64_t n_node_total;        // module nodes of the present modules (CSR)
   int32_t n_present;
   const int64_t* node_off;     // [n_present + 1]
-  const int32_t* node_mod;     // [n_node_total] module of each CSR node
-  const int32_t* node_order;   // [n_node_total] CSR nodes by module size (descending)
+  const int32_t* mod_order;    // [n_present] modules by size, descending
   const int64_t* cv_off;       // [n_present + 1] CorrVector offsets
   const double* disc_cv;       // discovery CorrVector (NULL: no CorrVector statistics)
   int64_t n_cv;                // its length
@@ -141,16 +140,15 @@ struct SweepParams {
   int32_t* col;                // [n_occ] test column of each (permutation, node)
   uint32_t* sorted;            // [n_occ] per item: (column << 16 | position), sorted by column
   int32_t* rank;               // [n_occ] sorted rank of each position
-  int32_t* count;              // [n_nodes] occurrences per column (then the scatter cursor)
+  int32_t* count;              // [n_nodes] occurrences per column
   int32_t* col_off;            // [n_nodes + 1]
   const double* zero;          // >= 32 zero bytes: the address of a lane with nothing to load
   double* sink;                // [128] the address of a lane with nothing to store
   double* dabs;                // [n_nodes] |diagonal| of each column with occurrences (written by the sweep)
-  int32_t* bnd;                // [items x (n_chunks + 1)] first sorted entry of each chunk
-  double* ys;                  // [items] CorrVector shift of the test side
-  uint4* meta;                 // [n_occ] by column slot: item base, jj | rank << 16, CorrVector base, b1 | k << 16
+  int32_t* lrank;              // [n_occ] slot of each occurrence within its column
+  uint4* meta;                 // [n_occ x 2] by column slot: item base, jj | rank << 16, CorrVector base,
+                               //   b1 | k << 16; CorrVector shifts {module, item}
   uint32_t* bndh;              // [n_chunks x n_occ] by slot (more than two chunks): e0 | e1 << 16 of the chunk
-  double2* shiftv;             // [n_occ] by slot: CorrVector shifts {module, item} (CorrVector only)
   double* rec;                 // [n_occ x n_chunks x kSweepRec] one record per (occurrence, chunk)
   const int32_t* row_of;
   int32_t n_rows, n_stat;

@@ -17,17 +17,16 @@
 // (corr(idx[ii], idx[jj]) for ii > jj, src/netStats.cpp:196-201).
 //
 // Steps per batch (launch_sweep):
-//  1. sweep_prep_kernel   per item: the permuted test columns (the index
-//     source of the other kernels, GetRandomIdx src/utils.cpp:193-199), their
-//     sorted order (SortNodes, src/netStats.cpp:23-32) as packed (column,
-//     position) entries, each position's sorted rank, the entries' split over
-//     the column chunks, the CorrVector shift of the item; and the column
-//     histogram of the batch;
+//  1. sweep_cols_kernel   per item: the permuted test columns (the index
+//     source of the other kernels, GetRandomIdx src/utils.cpp:193-199), the
+//     column histogram of the batch and each occurrence's slot within its
+//     column (the atomics' return values; items in module-size order);
 //  2. sweep_scan_kernel   column offsets (exclusive scan of the histogram);
-//  3. sweep_scatter_kernel the occurrences bucketed by column (slots), large
-//     modules first, with what the sweep needs of each: the item's entry
-//     base, node position and rank, module, the item's entries in each
-//     chunk;
+//  3. sweep_prep_kernel   per item: the columns' sorted order (SortNodes,
+//     src/netStats.cpp:23-32) as packed (column, position) entries, each
+//     position's sorted rank, the entries' split over the column chunks, the
+//     CorrVector shift of the item, and each occurrence's slot record (what
+//     the sweep needs of it) written to its column's slot;
 //  4. sweep_column_kernel one workgroup per (column, chunk): the chunk in LDS,
 //     sixteen lanes per occurrence over the item's sorted entries in the
 //     chunk, the next occurrences' metadata and entries in flight while the
@@ -60,57 +59,43 @@ namespace nr {
 // Packed sorted entry: test column (high 16 bits), module position (low 16).
 __device__ __forceinline__ uint32_t sw_pack(uint32_t col, uint32_t pos) { return (col << 16) | pos; }
 
-// ---- 1. per item ----------------------------------------------------------
-// One 256-thread workgroup per item (p, m), item = p * n_present + m. LDS: the
-// item's k columns and the per-chunk counts.
-__global__ void __launch_bounds__(256) sweep_prep_kernel(SweepParams P) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* cols = reinterpret_cast<uint32_t*>(smem);  // [k]
-  __shared__ int s_cnt[kSweepMaxChunks];
-  const int64_t item = blockIdx.x;
-  const int64_t p = item / P.n_present;
-  const int m = (int)(item - p * P.n_present);
-  const int64_t off = P.node_off[m];
-  const int k = (int)(P.node_off[m + 1] - off);
-  const int64_t base = p * P.n_node_total + off;
+// Items run in module-size order, largest first: block b is module
+// mod_order[b / n_perm] of permutation b % n_perm, so the column slots handed
+// out by the atomics below fill roughly by module size, and the lane groups of
+// a sweep wave carry items of similar size. The slot order within a column is
+// whatever the atomics give; every record is per occurrence, so the results
+// do not depend on it.
+struct SwItem {
+  int64_t p, item, off, base;
+  int m, k;
+};
+__device__ __forceinline__ SwItem sw_item(const SweepParams& P, int64_t b) {
+  SwItem it;
+  const int64_t mi = b / P.n_perm;
+  it.p = b - mi * P.n_perm;
+  it.m = P.mod_order[mi];
+  it.item = it.p * P.n_present + it.m;
+  it.off = P.node_off[it.m];
+  it.k = (int)(P.node_off[it.m + 1] - it.off);
+  it.base = it.p * P.n_node_total + it.off;
+  return it;
+}
+
+// ---- 1. per item: test columns, column histogram, slots within columns ------
+__global__ void __launch_bounds__(256) sweep_cols_kernel(SweepParams P) {
+  const SwItem it = sw_item(P, blockIdx.x);
   nr_prp_key key;
-  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + p), P.src.n_null);
-  for (int i = threadIdx.x; i < kSweepMaxChunks; i += 256) s_cnt[i] = 0;
-  for (int c = threadIdx.x; c < k; c += 256) cols[c] = node_index(P.src, key, p, off + c);
-  __syncthreads();
-  for (int c = threadIdx.x; c < k; c += 256) {
-    const uint32_t ic = cols[c];
-    int r = 0;
-    for (int q = 0; q < k; ++q) r += cols[q] < ic;  // distinct columns: one shuffle per permutation
-    P.sorted[base + r] = sw_pack(ic, (uint32_t)c);
-    P.rank[base + c] = r;
-    P.col[base + c] = (int32_t)ic;
-    atomicAdd(&P.count[ic], 1);
-    atomicAdd(&s_cnt[ic / P.chunk_rows], 1);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    int32_t* b = P.bnd + item * (P.n_chunks + 1);
-    for (int h = 0; h < P.n_chunks; ++h) {
-      b[h] = acc;
-      acc += s_cnt[h];
-    }
-    b[P.n_chunks] = acc;
-    // CorrVector shift of the test side: the item's first pair (net_item)
-    double ys = 0.0;
-    if (k > 1) {
-      const double y0 = P.pairs[((int64_t)cols[1] + (int64_t)cols[0] * P.n_nodes) * P.es].x;
-      ys = isfinite(y0) ? y0 : 0.0;
-    }
-    P.ys[item] = ys;
+  if (P.src.mode == NR_IDX_PRP) key = nr_prp_make_key(P.src.seed, (uint64_t)(P.src.perm_base + it.p), P.src.n_null);
+  for (int c = threadIdx.x; c < it.k; c += 256) {
+    const int32_t ic = node_index(P.src, key, it.p, it.off + c);
+    P.col[it.base + c] = ic;
+    P.lrank[it.base + c] = atomicAdd(&P.count[ic], 1);
   }
 }
 
 // ---- 2. column offsets ------------------------------------------------------
-// One 1024-thread workgroup: off[c] = sum of count[< c]; count becomes the
-// scatter cursor (zeroed).
-__global__ void __launch_bounds__(1024) sweep_scan_kernel(int32_t* count, int32_t* off, int64_t n) {
+// One 1024-thread workgroup: off[c] = sum of count[< c].
+__global__ void __launch_bounds__(1024) sweep_scan_kernel(const int32_t* count, int32_t* off, int64_t n) {
   __shared__ int32_t s[1024];
   const int t = threadIdx.x;
   const int64_t per = (n + 1023) / 1024;
@@ -127,48 +112,65 @@ __global__ void __launch_bounds__(1024) sweep_scan_kernel(int32_t* count, int32_
   }
   int32_t run = s[t] - sum;  // exclusive prefix of this thread's range
   for (int64_t i = a; i < b; ++i) {
-    const int32_t c = count[i];
     off[i] = run;
-    run += c;
-    count[i] = 0;
+    run += count[i];
   }
   if (t == 1023) off[n] = s[t];
 }
 
-// ---- 3. occurrences by column ------------------------------------------------
-// Threads walk blocks of 64 nodes in node_order (modules by size, descending)
-// and, per block, every permutation: consecutive threads read consecutive
-// nodes of one permutation, and each column's slots fill roughly in module-size
-// order, so the lane groups of a sweep wave carry items of similar size. The
-// slot order within a column is whatever the atomics give; every record is
-// per occurrence, so the results do not depend on it.
-__global__ void sweep_scatter_kernel(SweepParams P) {
-  const int64_t nt = P.n_node_total;
-  const int64_t per_block = 64 * (int64_t)P.n_perm;
-  const int64_t total = (nt + 63) / 64 * per_block;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t rb = t / per_block;
-    const int64_t rem = t - rb * per_block;
-    const int64_t p = rem >> 6;
-    const int64_t r = rb * 64 + (rem & 63);
-    if (r >= nt) continue;
-    const int32_t node = P.node_order[r];
-    const int64_t o = p * nt + node;
-    const int32_t c = P.col[o];
-    const int32_t s = P.col_off[c] + atomicAdd(&P.count[c], 1);
-    const int m = P.node_mod[node];
-    const int64_t off = P.node_off[m];
-    const uint32_t k = (uint32_t)(P.node_off[m + 1] - off);
-    const uint32_t jj = (uint32_t)(node - off);
-    const int64_t item = p * P.n_present + m;
-    const int32_t* b = P.bnd + item * (P.n_chunks + 1);
-    // CorrVector base of jj's pairs: v(ii, jj) = cv_off + jj (2k - jj - 1) / 2 + ii - jj - 1
-    const uint32_t cvb = P.disc_cv ? (uint32_t)(P.cv_off[m] + (int64_t)jj * (2 * (int64_t)k - jj - 1) / 2 - jj - 1) : 0u;
-    P.meta[s] = make_uint4((uint32_t)(p * nt + off), jj | ((uint32_t)P.rank[o] << 16), cvb,
-                           (P.n_chunks > 1 ? (uint32_t)b[1] : k) | (k << 16));
+// ---- 3. per item: sorted entries, chunk split, occurrences into their slots --
+// One 256-thread workgroup per item. LDS: the item's k columns and sorted
+// ranks, the per-chunk counts. Each occurrence's 32-byte slot record (what
+// the sweep needs of it) goes to its column's slot: item entry base, jj |
+// rank << 16, CorrVector base of jj's pairs, b1 | k << 16 (the first entry of
+// chunk 1 and the item size: the range of a one- or two-chunk sweep; more
+// chunks write bndh), then the CorrVector shifts {discovery (module), test
+// (item)}.
+__global__ void __launch_bounds__(256) sweep_prep_kernel(SweepParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const SwItem it = sw_item(P, blockIdx.x);
+  const int k = it.k;
+  uint32_t* cols = reinterpret_cast<uint32_t*>(smem);  // [k]
+  int32_t* rnk = reinterpret_cast<int32_t*>(smem) + k;  // [k]
+  __shared__ int s_cnt[kSweepMaxChunks + 1];
+  __shared__ double s_ys;
+  for (int i = threadIdx.x; i <= kSweepMaxChunks; i += 256) s_cnt[i] = 0;
+  for (int c = threadIdx.x; c < k; c += 256) cols[c] = (uint32_t)P.col[it.base + c];
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += 256) {
+    const uint32_t ic = cols[c];
+    int r = 0;
+    for (int q = 0; q < k; ++q) r += cols[q] < ic;  // distinct columns: one shuffle per permutation
+    P.sorted[it.base + r] = sw_pack(ic, (uint32_t)c);
+    P.rank[it.base + c] = r;
+    rnk[c] = r;
+    atomicAdd(&s_cnt[ic / P.chunk_rows + 1], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int h = 0; h < P.n_chunks; ++h) s_cnt[h + 1] += s_cnt[h];  // s_cnt[h] = first entry of chunk h
+    // CorrVector shift of the test side: the item's first pair (net_item)
+    double ys = 0.0;
+    if (k > 1) {
+      const double y0 = P.pairs[((int64_t)cols[1] + (int64_t)cols[0] * P.n_nodes) * P.es].x;
+      ys = isfinite(y0) ? y0 : 0.0;
+    }
+    s_ys = ys;
+  }
+  __syncthreads();
+  const uint32_t b1 = P.n_chunks > 1 ? (uint32_t)s_cnt[1] : (uint32_t)k;
+  const double xs = P.cv_shift ? P.cv_shift[it.m] : 0.0;
+  const int64_t cvo = P.disc_cv ? P.cv_off[it.m] : 0;
+  for (int c = threadIdx.x; c < k; c += 256) {
+    const int32_t s = P.col_off[cols[c]] + P.lrank[it.base + c];
+    // CorrVector base of c's pairs: v(ii, c) = cv_off + c (2k - c - 1) / 2 + ii - c - 1
+    const uint32_t cvb = P.disc_cv ? (uint32_t)(cvo + (int64_t)c * (2 * (int64_t)k - c - 1) / 2 - c - 1) : 0u;
+    uint4* mt = P.meta + 2 * (int64_t)s;
+    mt[0] = make_uint4((uint32_t)it.base, (uint32_t)c | ((uint32_t)rnk[c] << 16), cvb, b1 | ((uint32_t)k << 16));
+    if (P.disc_cv) mt[1] = __builtin_bit_cast(uint4, make_double2(xs, s_ys));
     if (P.n_chunks > 2)
-      for (int h = 0; h < P.n_chunks; ++h) P.bndh[(int64_t)h * P.n_occ + s] = (uint32_t)b[h] | ((uint32_t)b[h + 1] << 16);
-    if (P.shiftv) P.shiftv[s] = make_double2(P.cv_shift ? P.cv_shift[m] : 0.0, P.ys[item]);
+      for (int h = 0; h < P.n_chunks; ++h)
+        P.bndh[(int64_t)h * P.n_occ + s] = (uint32_t)s_cnt[h] | ((uint32_t)s_cnt[h + 1] << 16);
   }
 }
 
@@ -228,7 +230,7 @@ typedef unsigned int sw_u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kSwOff = 0xFFFFFFF0u;  // past every descriptor's range: reads 0
 
 struct SwRsrc {
-  __amdgpu_buffer_rsrc_t meta, bndh, shift, sorted, dcv;
+  __amdgpu_buffer_rsrc_t meta, bndh, sorted, dcv;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sw_rsrc(const void* p, int64_t bytes) {
@@ -241,11 +243,13 @@ template <bool X>
 __device__ __forceinline__ void sw_fetch(const SweepParams& P, const SwRsrc& R, int h, int32_t s, int32_t o1,
                                          SwOcc& q) {
   const bool in = s < o1;
-  q.mt = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(R.meta, in ? (uint32_t)s * 16u : kSwOff, 0, 0));
+  q.mt = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(R.meta, in ? (uint32_t)s * 32u : kSwOff, 0, 0));
   q.bd = P.n_chunks > 2
              ? __builtin_amdgcn_raw_buffer_load_b32(R.bndh, in ? ((uint32_t)h * (uint32_t)P.n_occ + (uint32_t)s) * 4u : kSwOff, 0, 0)
              : 0u;
-  if (X) q.sh = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(R.shift, in ? (uint32_t)s * 16u : kSwOff, 0, 0));
+  if (X)
+    q.sh = __builtin_bit_cast(double2,
+                              __builtin_amdgcn_raw_buffer_load_b128(R.meta, in ? (uint32_t)s * 32u + 16u : kSwOff, 0, 0));
 }
 
 // The chunk range e0 | e1 << 16 (from mt.w unless read from bndh).
@@ -419,9 +423,8 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int grp = lane / kSweepLanes, gl = lane % kSweepLanes;
   SwRsrc R;
-  R.meta = sw_rsrc(P.meta, P.n_occ * 16);
+  R.meta = sw_rsrc(P.meta, P.n_occ * 32);
   R.bndh = sw_rsrc(P.bndh, P.n_chunks > 2 ? P.n_occ * 4 * P.n_chunks : 0);
-  R.shift = sw_rsrc(P.shiftv, X ? P.n_occ * 16 : 0);
   R.sorted = sw_rsrc(P.sorted, P.n_occ * 4);
   R.dcv = sw_rsrc(P.disc_cv, X ? P.n_cv * 8 : 0);
   SwOcc cur, nxt;
@@ -595,19 +598,17 @@ hipError_t launch_sweep(const SweepParams& P0, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   if (P.n_occ != (int64_t)P.n_perm * P.n_node_total || P.n_chunks < 1 || P.n_chunks > kSweepMaxChunks ||
       P.chunk_rows * P.n_chunks < P.n_nodes || P.chunk_rows * (P.disc_cv ? 16 : 8) > kSweepChunkBytes ||
-      P.n_occ * 16 >= ((int64_t)1 << 32) || P.n_occ * 4 * P.n_chunks >= ((int64_t)1 << 32) ||
+      P.n_occ * 32 >= ((int64_t)1 << 32) || P.n_occ * 4 * P.n_chunks >= ((int64_t)1 << 32) ||
       P.n_cv * 8 >= ((int64_t)1 << 32))
     return hipErrorInvalidValue;  // the buffer descriptors' 32-bit byte offsets
   hipError_t e = hipMemsetAsync(P.count, 0, sizeof(int32_t) * (size_t)P.n_nodes, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sweep_prep_kernel, dim3((unsigned)n_items), dim3(256), sizeof(uint32_t) * (size_t)P.k_max, st,
-                     P);
+  hipLaunchKernelGGL(sweep_cols_kernel, dim3((unsigned)n_items), dim3(256), 0, st, P);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sweep_scan_kernel, dim3(1), dim3(1024), 0, st, P.count, P.col_off, P.n_nodes);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const int64_t n_thr = (P.n_node_total + 63) / 64 * 64 * (int64_t)P.n_perm;
-  const unsigned gs = (unsigned)std::min<int64_t>((n_thr + 255) / 256, 16384);
-  hipLaunchKernelGGL(sweep_scatter_kernel, dim3(gs), dim3(256), 0, st, P);
+  hipLaunchKernelGGL(sweep_prep_kernel, dim3((unsigned)n_items), dim3(256), 2 * sizeof(uint32_t) * (size_t)P.k_max, st,
+                     P);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const dim3 grid((unsigned)P.n_nodes, (unsigned)P.n_chunks);
   if (P.disc_cv && P.finite)
