@@ -412,11 +412,14 @@ int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol);
  * once per pair, R/networkProperties.R:295-302): the discovery dataset of
  * netrep_IntermediateProperties and the dataset of netrep_NetProps stay
  * resident in HBM while later calls name the same host arrays (same
- * pointers and shape, and the same sampled fingerprint of their contents);
- * contexts (streams, slot scratch) are pooled across calls. The arrays must
- * not change between calls that should reuse them. netrep_ReleaseResident
- * frees all of it (the R glue calls it when modulePreservation /
- * networkProperties return). */
+ * pointers and shape, and the same fingerprint of every element, hashed on
+ * the call's host threads); contexts (streams, slot scratch) are pooled
+ * across calls, and a pooled context is reset to the defaults (no dataset,
+ * no cancel request, the process-wide host-thread count). A changed array
+ * is uploaded again. netrep_ReleaseResident frees all of it (the R glue calls
+ * it when modulePreservation / networkProperties return); a
+ * netrep_PermutationProcedure call that runs out of device memory releases
+ * the resident datasets and retries once before returning NR_ERR_OOM. */
 void netrep_ReleaseResident(void);
 
 /* Last error of the reference-interface layer (thread-local). */
