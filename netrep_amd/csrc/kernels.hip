@@ -1801,6 +1801,12 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
         gram_mfma<NW, PACKED>(X, S, L.idx, k, P.ones_off, G, G32, ld, g1[0], bad);
     }
     if (bad) atomicOr(&s_flags[1], 1);
+#ifdef NR_GRAM_ONLY
+    // diagnostic build only (make EXTRA=-DNR_GRAM_ONLY=1 OUT=...): the Gram
+    // phase alone, for its counters; every item then takes the non-finite
+    // path (NA statistics), so nothing after the Gram runs
+    if (tid == 0) atomicOr(&s_flags[1], 1);
+#endif
     block_sums<1, NW>(g1, L.red);  // barriers also publish G to the whole workgroup
     NR_STAMP(1);  // Gram
     if (s_flags[1] == 0) {
