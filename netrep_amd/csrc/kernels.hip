@@ -990,6 +990,9 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
   const int T4 = (kc + 63) / 64;
   const int nsup = T4 * (T4 + 1) / 2;
   const int full = S / 16 * 16;  // primal: steps whose 16 rows are all in range
+  // (Four waves on a 2 x 2 block of super-tiles instead of a row of four
+  // read 4 operand panels per round instead of 5, but idle a wave in every
+  // diagonal block: C5 profile kernel 56.6 vs 53.6 ms, profiles/r05/g64ab/.)
   for (int t = wave; t < nsup; t += NW) {
     int I4 = 0, rem = t;
     while (rem >= T4 - I4) { rem -= T4 - I4; ++I4; }
