@@ -132,7 +132,7 @@ struct nr_ctx {
     uint32_t *sorted = nullptr, *bndh = nullptr;
     uint4* meta = nullptr;
     double *rec = nullptr, *dabs = nullptr;
-    double* zs = nullptr;  // [4] zeros + [128] sink (sweep.hip: lanes with nothing to load / store)
+    double* zs = nullptr;  // [4] zeros + [256] sink (sweep.hip: lanes with nothing to load / store)
     size_t occ_cap = 0, col_cap = 0;
     int32_t chunk_cap = 0;
   } sweep[2];
@@ -650,7 +650,7 @@ int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const
     b.chunk_cap = P.n_chunks;
   }
   if (!b.zs) {
-    NR_HIP(ctx, hipMalloc((void**)&b.zs, (4 + 128) * sizeof(double)));
+    NR_HIP(ctx, hipMalloc((void**)&b.zs, (4 + 256) * sizeof(double)));
     NR_HIP(ctx, hipMemsetAsync(b.zs, 0, 4 * sizeof(double), ln.st));
   }
   const size_t n_cols = (size_t)ctx->n_nodes + 1;

@@ -111,7 +111,7 @@ struct ProfileParams {
 // test column (each column chunk streamed into LDS once, every occurrence of
 // the column reads its rows there) instead of one random gather per pair.
 constexpr int kSweepWaves = 16;                   // waves per (column, chunk) workgroup: one per CU
-constexpr int kSweepLanes = 16;                   // lanes per occurrence
+constexpr int kSweepLanes = 8;                    // lanes per occurrence (16: 2-5% slower, r05/l8b)
 constexpr int kSweepMaxChunks = 16;               // chunks per column (n <= 65,535)
 constexpr int kSweepMaxK = 4096;                  // module nodes (LDS of the per-item kernels)
 constexpr int64_t kSweepChunkBytes = 160000;      // LDS per (column, chunk) workgroup
@@ -143,7 +143,7 @@ struct SweepParams {
   int32_t* count;              // [n_nodes] occurrences per column
   int32_t* col_off;            // [n_nodes + 1]
   const double* zero;          // >= 32 zero bytes: the address of a lane with nothing to load
-  double* sink;                // [128] the address of a lane with nothing to store
+  double* sink;                // [256] the address of a lane with nothing to store
   double* dabs;                // [n_nodes] |diagonal| of each column with occurrences (written by the sweep)
   int32_t* lrank;              // [n_occ] slot of each occurrence within its column
   uint4* meta;                 // [n_occ x 2] by column slot: item base, jj | rank << 16, CorrVector base,

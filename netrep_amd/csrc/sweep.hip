@@ -28,7 +28,7 @@
 //     CorrVector shift of the item, and each occurrence's slot record (what
 //     the sweep needs of it) written to its column's slot;
 //  4. sweep_column_kernel one workgroup per (column, chunk): the chunk in LDS,
-//     sixteen lanes per occurrence over the item's sorted entries in the
+//     eight lanes per occurrence over the item's sorted entries in the
 //     chunk, the next occurrences' metadata and entries in flight while the
 //     current ones are summed; one partial record (weighted-degree parts,
 //     CorrVector sums) per (occurrence, chunk);
@@ -182,32 +182,43 @@ __device__ __forceinline__ unsigned long long sw_dpp_u64(unsigned long long v) {
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// Sums of v[0..16) over the 16 lanes of each row, transposed: afterwards lane
-// gl of the row holds the total of v[gl]. Four DPP exchange levels on lane
-// bits 3..0, halving the values at each (15 exchanges, not 64); fixed order.
-__device__ __forceinline__ double sw_transpose16(const double (&v)[16], int lane) {
-  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
-  double a8[8], a4[4], a2[2];
+// Eight-lane groups: the same exchanges over lane bits 2..0 (mirror within
+// 8, XOR 2, XOR 1), 16 values -> 2 per lane: lane bits (b2 b1 b0) hold the
+// totals of v[8 b2 + 4 b1 + 2 b0] and the next one.
+__device__ __forceinline__ double2 sw_transpose16_8(const double (&v)[16], int lane) {
+  const bool b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+  double a8[8], a4[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) a8[i] = (b3 ? v[i + 8] : v[i]) + nr_dpp<NR_DPP_ROR8>(b3 ? v[i] : v[i + 8]);
+  for (int i = 0; i < 8; ++i)  // lane ^ 7
+    a8[i] = (b2 ? v[i + 8] : v[i]) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? v[i] : v[i + 8]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)  // lane ^ 7: the partner's bits 1, 0 differ too; later levels cover them
-    a4[i] = (b2 ? a8[i + 4] : a8[i]) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? a8[i] : a8[i + 4]);
+  for (int i = 0; i < 4; ++i) a4[i] = (b1 ? a8[i + 4] : a8[i]) + nr_dpp<NR_DPP_XOR2>(b1 ? a8[i] : a8[i + 4]);
+  double2 r;
+  r.x = (b0 ? a4[2] : a4[0]) + nr_dpp<NR_DPP_XOR1>(b0 ? a4[0] : a4[2]);
+  r.y = (b0 ? a4[3] : a4[1]) + nr_dpp<NR_DPP_XOR1>(b0 ? a4[1] : a4[3]);
+  return r;
+}
+// ... and four integer sums over 8 lanes: lane bits (b2 b1) hold v[2 b2 + b1].
+__device__ __forceinline__ unsigned long long sw_transpose4_u64_8(const unsigned long long (&v)[4], int lane) {
+  const bool b2 = lane & 4, b1 = lane & 2;
+  unsigned long long a2[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) a2[i] = (b2 ? v[i + 2] : v[i]) + sw_dpp_u64<NR_DPP_HALF_MIRROR>(b2 ? v[i] : v[i + 2]);
+  unsigned long long x = (b1 ? a2[1] : a2[0]) + sw_dpp_u64<NR_DPP_XOR2>(b1 ? a2[0] : a2[1]);
+  return x + sw_dpp_u64<NR_DPP_XOR1>(x);
+}
+
+// Eight sums (the finite-data record: no pair count) over the 8 lanes: three
+// exchange levels leave each lane one total, of v[4 b2 + 2 b1 + b0].
+__device__ __forceinline__ double sw_transpose8_8(const double (&v)[8], int lane) {
+  const bool b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+  double a4[4], a2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    a4[i] = (b2 ? v[i + 4] : v[i]) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? v[i] : v[i + 4]);
 #pragma unroll
   for (int i = 0; i < 2; ++i) a2[i] = (b1 ? a4[i + 2] : a4[i]) + nr_dpp<NR_DPP_XOR2>(b1 ? a4[i] : a4[i + 2]);
   return (b0 ? a2[1] : a2[0]) + nr_dpp<NR_DPP_XOR1>(b0 ? a2[0] : a2[1]);
-}
-
-// The same for four exact integer sums: lanes with bits (3, 2) = (i, j) hold
-// the total of v[2i + j].
-__device__ __forceinline__ unsigned long long sw_transpose4_u64(const unsigned long long (&v)[4], int lane) {
-  const bool b3 = lane & 8, b2 = lane & 4;
-  unsigned long long a2[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) a2[i] = (b3 ? v[i + 2] : v[i]) + sw_dpp_u64<NR_DPP_ROR8>(b3 ? v[i] : v[i + 2]);
-  unsigned long long x = (b2 ? a2[1] : a2[0]) + sw_dpp_u64<NR_DPP_HALF_MIRROR>(b2 ? a2[0] : a2[1]);
-  x += sw_dpp_u64<NR_DPP_XOR2>(x);
-  return x + sw_dpp_u64<NR_DPP_XOR1>(x);
 }
 
 constexpr int kSweepPre = 6;  // entries per lane in flight per occurrence (4 / 8: r05/sweep A/B)
@@ -354,7 +365,7 @@ __device__ __forceinline__ void sw_block(const void* colv_, int64_t row0, const 
       const double xo = FIN ? x : (ok ? x : 0.0);
       const double yo = FIN ? w * yc : (ok ? yc : 0.0);
       const double dx = fma(-w, q.sh.x, xo), dy = fma(-w, q.sh.y, yo);  // x - xs, y - ys (exact products)
-      A.a[0] += w;
+      if (!FIN) A.a[0] += w;  // finite data: every pair complete, n = k (k - 1) / 2 (sweep_finish_kernel)
       A.a[1] += dx;
       A.a[2] += dy;
       A.a[3] += dx * dx;
@@ -374,7 +385,7 @@ __device__ __forceinline__ void sw_block(const void* colv_, int64_t row0, const 
 
 // One workgroup of kSweepWaves waves per (column c, chunk h): the chunk's rows
 // of column c in LDS ({corr, net} with CorrVector statistics, net alone
-// without); each wave takes four occurrences at a time, sixteen lanes per
+// without); each wave takes eight occurrences at a time, eight lanes per
 // occurrence over the item's sorted entries in the chunk; one partial record
 // per (occurrence, chunk), summed in chunk order by sweep_finish_kernel. The
 // next batch's entries and the one after's metadata load while a batch is
@@ -438,11 +449,14 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
   // store issued last would hold up the next wait for a prefetched load)
   double* st_d = P.sink + lane;
   unsigned long long* st_i = reinterpret_cast<unsigned long long*>(P.sink) + 64 + lane;
+  double2* st_d2 = reinterpret_cast<double2*>(P.sink + 128) + lane;
   double ds = 0.0;
+  double2 ds2 = make_double2(0.0, 0.0);
   unsigned long long is = 0;
   for (; sb < o1; sb += stride) {  // wave-uniform
     *st_d = ds;
     *st_i = is;
+    if constexpr (!FIN) *st_d2 = ds2;
     const uint32_t bdc = sw_range(P, cur, h);
     double xv[kSweepPre];
     if (X) sw_xv(R, cur, uc, xv);
@@ -461,19 +475,39 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
         sw_block<X, FIN>(colv, row0, cur, bdc, gl, t0, ux, xv, gj, A);
       }
     }
-    const double dv[16] = {A.plain, A.ff, A.a[0], A.a[1], A.a[2], A.a[3], A.a[4], A.a[5], A.a[6], 0, 0, 0, 0, 0, 0, 0};
+    // record fields: 0 plain, 1 ff, 2..7 the CorrVector sums sx, sy, sxx, syy,
+    // sxy, sum sign(x) y, 8 their pair count (not written for finite data),
+    // 9..11 the fixed-point parts
+    const double dv[16] = {A.plain, A.ff, A.a[1], A.a[2], A.a[3], A.a[4], A.a[5], A.a[6], A.a[0], 0, 0, 0, 0, 0, 0, 0};
+    const double dv8[8] = {A.plain, A.ff, A.a[1], A.a[2], A.a[3], A.a[4], A.a[5], A.a[6]};
     const bool same = (((cur.mt.y >> 16) ^ ((bdc & 0xFFFFu) + (uint32_t)gl)) & 1u) == 0;
     const unsigned long long iv[4] = {same ? A.fine : 0ull, same ? 0ull : A.fine, A.tn, 0};
-    ds = sw_transpose16(dv, lane);
-    is = sw_transpose4_u64(iv, lane);
     // the record by occurrence (item entry base + jj), so the finish kernel
-    // reads an item's records contiguously; lane gl < 9 stores double field
-    // gl, lanes 0, 4, 8 the integer fields 9..11, the others P.sink
+    // reads an item's records contiguously; lanes with nothing to store
+    // write P.sink
     const bool live = sb + grp < o1;
     double* rec = P.rec + ((int64_t)(cur.mt.x + (cur.mt.y & 0xFFFFu)) * P.n_chunks + h) * kSweepRec;
-    st_d = live && gl < 9 ? rec + gl : P.sink + lane;
-    st_i = live && (gl & 3) == 0 && gl < 12 ? reinterpret_cast<unsigned long long*>(rec) + 9 + (gl >> 2)
-                                             : reinterpret_cast<unsigned long long*>(P.sink) + 64 + lane;
+    if constexpr (FIN) {
+      // lane (b2 b1 b0): double field 4 b2 + 2 b1 + b0; lanes with b0 = 0: integer field 9 + 2 b2 + b1
+      ds = sw_transpose8_8(dv8, lane);
+      is = sw_transpose4_u64_8(iv, lane);
+      const int fi = 2 * ((gl >> 2) & 1) + ((gl >> 1) & 1);
+      st_d = live ? rec + gl : P.sink + lane;
+      st_i = live && (gl & 1) == 0 && fi < 3 ? reinterpret_cast<unsigned long long*>(rec) + 9 + fi
+                                              : reinterpret_cast<unsigned long long*>(P.sink) + 64 + lane;
+    } else {
+      // lane (b2 b1 b0): double fields 8 b2 + 4 b1 + 2 b0 and the next (field 8
+      // alone: 9 is an integer field); lanes with b0 = 0: integer field 9 + 2 b2 + b1
+      ds2 = sw_transpose16_8(dv, lane);
+      ds = ds2.x;
+      is = sw_transpose4_u64_8(iv, lane);
+      const int f0 = 8 * ((gl >> 2) & 1) + 4 * ((gl >> 1) & 1) + 2 * (gl & 1);
+      const int fi = 2 * ((gl >> 2) & 1) + ((gl >> 1) & 1);
+      st_d2 = live && f0 < 8 ? reinterpret_cast<double2*>(rec + f0) : reinterpret_cast<double2*>(P.sink + 128) + lane;
+      st_d = live && f0 == 8 ? rec + 8 : P.sink + lane;
+      st_i = live && (gl & 1) == 0 && fi < 3 ? reinterpret_cast<unsigned long long*>(rec) + 9 + fi
+                                              : reinterpret_cast<unsigned long long*>(P.sink) + 64 + lane;
+    }
     cur = nxt;
     nxt = nn;
 #pragma unroll
@@ -481,6 +515,7 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
   }
   *st_d = ds;
   *st_i = is;
+  if constexpr (!FIN) *st_d2 = ds2;
 }
 
 // ---- 5. per item ---------------------------------------------------------------
@@ -527,7 +562,8 @@ __global__ void __launch_bounds__(256) sweep_finish_kernel(SweepParams P, int64_
       plain += rec[0];
       ff += rec[1];
 #pragma unroll
-      for (int i = 0; i < 7; ++i) acc[i] += rec[2 + i];
+      for (int i = 1; i < 7; ++i) acc[i] += rec[1 + i];
+      if (!P.finite) acc[0] += rec[8];
       pb += irec[9];
       on += irec[10];
       tn += irec[11];
@@ -545,6 +581,7 @@ __global__ void __launch_bounds__(256) sweep_finish_kernel(SweepParams P, int64_
   }
 #pragma unroll
   for (int i = 0; i < 7; ++i) acc[i] = nr_wave_sum(acc[i]);
+  if (P.finite) acc[0] = 0.5 * (double)k * (double)(k - 1);  // finite data: every pair complete
 #pragma unroll
   for (int i = 0; i < 4; ++i) a1[i] = nr_wave_sum(a1[i]);
   const double mx = a1[2] / a1[1], my = a1[3] / a1[1];

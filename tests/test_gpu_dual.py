@@ -145,3 +145,18 @@ def test_lanczos_dimension_beyond_lds_vectors(sizes, n_samples, seed, n_nodes):
     exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
     assert_stats_close(eng.observed(), obs, what=f"observed (k {sizes[0]}, S {n_samples})")
     assert_stats_close(nulls, exp, what=f"nulls (k {sizes[0]}, S {n_samples})")
+
+
+def test_lanczos_beyond_lds_mixed_sizes_multi_slot():
+    """a variant-6 module (Lanczos dimension 2,600 > the LDS
+    vectors, every vector in its slot's scratch) in a multi-permutation run
+    beside a 350-node module (the runtime-layout class) and two packed-class
+    modules: six permutations put six variant-6 items in flight on six slots
+    of one launch. Against the C++ LAPACK restatement on identical shuffles."""
+    lay, mi, disc, txs, tc, tn = _case([2700, 350, 90, 35], 2600, 97, n_nodes=4000)
+    eng = _engine_from(mi, disc, txs, tc, tn)
+    nulls = eng.run(0, 6, 29)
+    pis = N.prp_table(29, 0, 6, mi.null_idx.size)
+    exp, obs = _cpp(mi, disc, txs, tc, tn, pis)
+    assert_stats_close(eng.observed(), obs, what="observed (mixed sizes, variant 6)")
+    assert_stats_close(nulls, exp, what="nulls (mixed sizes, variant 6)")
