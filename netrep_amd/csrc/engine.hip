@@ -609,11 +609,18 @@ int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std
 // occurrence ids, bounded buffers); an item's statistics do not depend on
 // the batch it runs in, so neither do the results.
 constexpr int64_t kSweepMaxOcc = (int64_t)64 << 20;
+constexpr int64_t kSweepMaxRecBytes = (int64_t)32 << 30;  // the (occurrence, chunk) records of one sub-batch
 
 int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const Lane& ln);
 
 int launch_sweep_batch(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const Lane& ln) {
-  const int64_t per = std::max<int64_t>(1, kSweepMaxOcc / std::max<int64_t>(ctx->n_node_total, 1));
+  // occurrences per sub-batch: at most kSweepMaxOcc, and records of at most
+  // kSweepMaxRecBytes (many column chunks at large n)
+  const int64_t chunks =
+      (ctx->n_nodes + nr::sweep_chunk_rows(ctx->n_nodes, np.disc_cv ? 16 : 8) - 1) /
+      nr::sweep_chunk_rows(ctx->n_nodes, np.disc_cv ? 16 : 8);
+  const int64_t max_occ = std::min<int64_t>(kSweepMaxOcc, kSweepMaxRecBytes / (chunks * 8 * nr::kSweepRec));
+  const int64_t per = std::max<int64_t>(1, max_occ / std::max<int64_t>(ctx->n_node_total, 1));
   for (int64_t p0 = 0; p0 < n_perm; p0 += per) {
     const int64_t np_sub = std::min(per, n_perm - p0);
     nr::NetParams q = np;
