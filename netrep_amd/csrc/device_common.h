@@ -29,6 +29,21 @@ __device__ __forceinline__ double nr_wave_max(double v);
 // Wave-wide sum (every lane active); register butterflies, see nr_wave_sum.
 __device__ __forceinline__ double wave_sum(double v) { return nr_wave_sum(v); }
 
+// Workgroup barrier of an NW-wave workgroup. One wave (the wave class): a
+// wavefront-scope fence only -- a wave's LDS and vector-memory operations are
+// performed in program order, so the s_barrier and the release fence's wait
+// for outstanding global stores (the Lanczos basis, the cube) are not needed.
+template <int NW>
+__device__ __forceinline__ void nr_sync() {
+  if constexpr (NW == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
 // Block-wide sums of N values; result broadcast to every thread. `red` must
 // hold N * NR_WAVES doubles of LDS. Contains two barriers (one with
 // TRAIL = false: then `red` must not be written again before a later barrier).
@@ -37,11 +52,12 @@ __device__ __forceinline__ void block_sums(double (&v)[N], double* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+  if constexpr (NW == 1) return;  // one wave: every lane has the sums (no LDS round trip)
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < N; ++i) red[i * NW + wave] = v[i];
   }
-  __syncthreads();
+  nr_sync<NW>();
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double s = 0.0;
@@ -49,7 +65,7 @@ __device__ __forceinline__ void block_sums(double (&v)[N], double* red) {
     for (int w = 0; w < NW; ++w) s += red[i * NW + w];
     v[i] = s;
   }
-  if (TRAIL) __syncthreads();
+  if (TRAIL) nr_sync<NW>();
 }
 
 // Pearson correlation from (shifted) one-pass sums over complete cases.
@@ -117,8 +133,14 @@ __device__ __forceinline__ double nr_rcp(double d) {
 // last lane sits exactly on that upper end -- finds eigenvalues above it;
 // then the search continues to the Gershgorin bound. Near convergence this
 // halves the passes of a check.
+//
+// wa, wb (n doubles of LDS each, or NULL): the normalised recurrence
+// coefficients alpha_i / scale and (beta_i / scale)^2, computed once per call
+// by the wave instead of in every pass (the passes are issue-bound: three
+// fewer instructions per step; the same products, so the same counts).
 static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha, const double* beta, int n, int lane,
-                                                            double theta_prev = 0.0, double r_prev = 0.0) {
+                                                            double theta_prev = 0.0, double r_prev = 0.0,
+                                                            double* wa = nullptr, double* wb = nullptr) {
   double lo = alpha[0], hi = alpha[0];
   for (int i = lane; i < n; i += 64) {
     const double r = (i > 0 ? fabs(beta[i - 1]) : 0.0) + (i < n - 1 ? fabs(beta[i]) : 0.0);
@@ -141,39 +163,74 @@ static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha,
     lo = theta_prev - 4e-16 * scale;
     hi = theta_prev + 1.01 * r_prev + 4e-16 * scale;
   }
+  if (wa) {
+    for (int i = lane; i < n; i += 64) {
+      wa[i] = alpha[i] * inv;
+      if (i < n - 1) {
+        const double b = beta[i] * inv;
+        wb[i] = b * b;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   for (int it = 0; it < 14; ++it) {
     // warm first pass: 64 points ending on hi; otherwise 64 interior points
     const double den = warm ? 64.0 : 65.0;
     const double x = (lo + (hi - lo) * (double)(lane + 1) / den) * inv;
     double p0 = 1.0, p1 = alpha[0] * inv - x;
     int cnt = p1 < 0.0;  // eigenvalues < x
-    // 8 steps' alpha/beta read ahead of their recurrence steps, so the LDS
+    // a sign change between p_{i-1} and p_i: the sign bits differ
+    auto step = [&](double a, double bb) {
+      const double p2 = fma(a - x, p1, -bb * p0);
+      cnt += (int)((__double2hiint(p2) ^ __double2hiint(p1)) >> 31 & 1);
+      p0 = p1;
+      p1 = p2;
+    };
+    auto renorm = [&]() {
+      const double mg = fabs(p1);
+      const double s = mg > 1e150 ? 1e-150 : (mg < 1e-150 ? 1e150 : 1.0);
+      p0 *= s;
+      p1 *= s;
+    };
+    // 8 steps' coefficients read ahead of their recurrence steps, so the LDS
     // latency is paid once per 8 steps instead of on the dependency chain of
-    // every step (same arithmetic in the same order)
-    for (int i0 = 1; i0 < n; i0 += 8) {
+    // every step (same arithmetic in the same order); whole groups of 8 carry
+    // no per-step bounds test (a single wave pays an issue slot for each)
+    int i0 = 1;
+    for (; i0 + 8 <= n; i0 += 8) {
       double av[8], bv[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        const int i = min(i0 + t, n - 1);
-        av[t] = alpha[i];
-        bv[t] = beta[i - 1];
+        const int i = i0 + t;
+        if (wa) {
+          av[t] = wa[i];
+          bv[t] = wb[i - 1];
+        } else {
+          av[t] = alpha[i] * inv;
+          const double b = beta[i - 1] * inv;
+          bv[t] = b * b;
+        }
       }
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        if (i0 + t < n) {
-          const double b = bv[t] * inv;
-          const double p2 = fma(av[t] * inv - x, p1, -(b * b) * p0);
-          cnt += (p2 < 0.0) != (p1 < 0.0);
-          p0 = p1;
-          p1 = p2;
-          if ((t & 3) == 3) {  // i = i0 + t with i0 = 1 mod 8: i = 0 mod 4
-            const double mg = fabs(p1);
-            const double s = mg > 1e150 ? 1e-150 : (mg < 1e-150 ? 1e150 : 1.0);
-            p0 *= s;
-            p1 *= s;
-          }
-        }
+        step(av[t], bv[t]);
+        if ((t & 3) == 3) renorm();  // i = i0 + t with i0 = 1 mod 8: i = 0 mod 4
       }
+    }
+    for (int i = i0; i < n; ++i) {
+      double a, bb;
+      if (wa) {
+        a = wa[i];
+        bb = wb[i - 1];
+      } else {
+        a = alpha[i] * inv;
+        const double b = beta[i - 1] * inv;
+        bb = b * b;
+      }
+      step(a, bb);
+      if ((i & 3) == 0) renorm();
     }
     // largest x with cnt <= n-1 becomes lo; smallest x with cnt == n becomes hi
     const unsigned long long below = __ballot(cnt <= n - 1);
@@ -224,72 +281,95 @@ static __device__ __forceinline__ double tri_top_resid(const double* alpha, cons
 
 // Eigenvector of the tridiagonal for eigenvalue theta by two steps of inverse
 // iteration; LU with partial pivoting as LAPACK dgttrf/dgtts2. Single lane.
-// y[0..n) comes back normalised; work holds 5n doubles.
-static __device__ __forceinline__ void tri_eigenvector(const double* alpha, const double* beta, int n, double theta,
-                                double* y, double* work) {
-  double* dl = work;
-  double* d = work + n;
-  double* du = work + 2 * n;
-  double* du2 = work + 3 * n;
-  double* swp = work + 4 * n;
+// y[0..n) comes back normalised; work holds 5n doubles. The recurrences carry
+// their running values in registers (the pivot, the super-diagonal, y_i and
+// y_{i+1}) and the pivots are stored as reciprocals, so each step's
+// dependency chain is one or two FMAs instead of an LDS round trip and a
+// division (round 5: a single-wave item had no other wave to hide the old
+// loop behind, 12% of a C2 item). The second step starts from the first
+// step's result scaled by 1/max (proportional to the normalised vector the
+// old loop passed on: the same direction to rounding).
+static __device__ __forceinline__ void tri_eigenvector(const double* __restrict__ alpha,
+                                                       const double* __restrict__ beta, int n, double theta,
+                                                       double* __restrict__ y, double* __restrict__ work) {
+  double* __restrict__ dl = work;
+  double* __restrict__ rd = work + n;   // 1 / pivot
+  double* __restrict__ du = work + 2 * n;
+  double* __restrict__ du2 = work + 3 * n;
+  double* __restrict__ swp = work + 4 * n;
   double scale = fabs(theta);
   for (int i = 0; i < n; ++i) {
-    d[i] = alpha[i] - theta;
     scale = fmax(scale, fabs(alpha[i]));
-    if (i < n - 1) {
-      du[i] = beta[i];
-      dl[i] = beta[i];
-      scale = fmax(scale, fabs(beta[i]));
-    }
-    du2[i] = 0.0;
-    swp[i] = 0.0;
+    if (i < n - 1) scale = fmax(scale, fabs(beta[i]));
   }
   const double floor_piv = 1e-300 + 2.2e-16 * scale;
+  double di = alpha[0] - theta;          // current pivot candidate d_i
+  double dui = n > 1 ? beta[0] : 0.0;    // current super-diagonal du_i
   for (int i = 0; i < n - 1; ++i) {
-    if (fabs(d[i]) >= fabs(dl[i])) {
-      if (fabs(d[i]) < floor_piv) d[i] = d[i] < 0.0 ? -floor_piv : floor_piv;
-      const double f = dl[i] / d[i];
+    const double bi = beta[i];                       // sub-diagonal dl_i
+    const double dn = alpha[i + 1] - theta;          // d_{i+1} before this step
+    const double dun = i < n - 2 ? beta[i + 1] : 0.0;  // du_{i+1} before this step
+    if (fabs(di) >= fabs(bi)) {
+      if (fabs(di) < floor_piv) di = di < 0.0 ? -floor_piv : floor_piv;
+      const double r = 1.0 / di;
+      const double f = bi * r;
       dl[i] = f;
-      d[i + 1] -= f * du[i];
-    } else {
-      const double f = d[i] / dl[i];
-      d[i] = dl[i];
+      rd[i] = r;
+      du[i] = dui;
+      du2[i] = 0.0;
+      swp[i] = 0.0;
+      di = dn - f * dui;
+      dui = dun;
+    } else {  // row interchange
+      const double r = 1.0 / bi;
+      const double f = di * r;
       dl[i] = f;
-      const double t = du[i];
-      du[i] = d[i + 1];
-      d[i + 1] = t - f * d[i + 1];
-      if (i < n - 2) {
-        du2[i] = du[i + 1];
-        du[i + 1] = -f * du[i + 1];
-      }
+      rd[i] = r;
+      du[i] = dn;
+      du2[i] = dun;
       swp[i] = 1.0;
+      di = dui - f * dn;
+      dui = -f * dun;
     }
   }
-  if (fabs(d[n - 1]) < floor_piv) d[n - 1] = d[n - 1] < 0.0 ? -floor_piv : floor_piv;
-  for (int i = 0; i < n; ++i) y[i] = 1.0;
+  if (fabs(di) < floor_piv) di = di < 0.0 ? -floor_piv : floor_piv;
+  rd[n - 1] = 1.0 / di;
+  double sc = 1.0;  // scale of the right-hand side (1 / max of the previous iterate)
   for (int iter = 0; iter < 2; ++iter) {
+    // L solve (the row interchanges applied as the factorisation made them)
+    double yi = iter == 0 ? 1.0 : y[0] * sc;
     for (int i = 0; i < n - 1; ++i) {
+      const double yn = iter == 0 ? 1.0 : y[i + 1] * sc;
+      const double f = dl[i];
       if (swp[i] == 0.0) {
-        y[i + 1] -= dl[i] * y[i];
+        y[i] = yi;
+        yi = yn - f * yi;
       } else {
-        const double t = y[i];
-        y[i] = y[i + 1];
-        y[i + 1] = t - dl[i] * y[i];
+        y[i] = yn;
+        yi = yi - f * yn;
       }
     }
-    y[n - 1] /= d[n - 1];
-    if (n > 1) y[n - 2] = (y[n - 2] - du[n - 2] * y[n - 1]) / d[n - 2];
-    for (int i = n - 3; i >= 0; --i) y[i] = (y[i] - du[i] * y[i + 1] - du2[i] * y[i + 2]) / d[i];
-    double mx = 0.0;
-    for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(y[i]));
-    double nrm = 0.0;
-    for (int i = 0; i < n; ++i) {
-      y[i] /= mx;
-      nrm += y[i] * y[i];
+    // U solve (bandwidth 3)
+    double y1 = yi * rd[n - 1], y2 = 0.0;
+    y[n - 1] = y1;
+    double mx = fabs(y1);
+    for (int i = n - 2; i >= 0; --i) {
+      const double y0 = (y[i] - du[i] * y1 - du2[i] * y2) * rd[i];
+      y[i] = y0;
+      mx = fmax(mx, fabs(y0));
+      y2 = y1;
+      y1 = y0;
     }
-    const double inv = 1.0 / sqrt(nrm);
-    for (int i = 0; i < n; ++i) y[i] *= inv;
+    sc = 1.0 / mx;
   }
+  double nrm = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double v = y[i] * sc;
+    y[i] = v;
+    nrm += v * v;
+  }
+  const double inv = 1.0 / sqrt(nrm);
+  for (int i = 0; i < n; ++i) y[i] *= inv;
 }
 
 // Partial reorthogonalisation (Simon 1984): omega_{j+1,i} estimates q_{j+1}.q_i
@@ -421,18 +501,39 @@ __device__ __forceinline__ uint64_t nr_clock() { return __builtin_amdgcn_s_memti
 // the stamps' live timer and branches change the profile kernel's register
 // allocation (its spills grew 212 -> 352 B/lane with four more stamp sites,
 // and the kernel ran 30% slower), so the shipped library carries none.
+// Each workgroup sums its phases in LDS and adds them to P.stamps once, at
+// the end of the kernel (round 5: one global atomic per stamp from every
+// workgroup contended on 16 addresses and inflated the per-step phases).
 #ifdef NR_STAMPS
+static __shared__ unsigned long long nr_stamp_acc[NR_N_STAMPS];
 #define NR_STAMP(slot)                                                          \
   do {                                                                          \
     if (P.stamps && threadIdx.x == 0) {                                         \
       const uint64_t t_ = nr_clock();                                           \
-      atomicAdd((unsigned long long*)&P.stamps[slot], (unsigned long long)(t_ - t_mark)); \
+      nr_stamp_acc[slot] += (unsigned long long)(t_ - t_mark);                  \
       t_mark = t_;                                                              \
     }                                                                           \
+  } while (0)
+#define NR_STAMP_INIT()                                                         \
+  do {                                                                          \
+    if (threadIdx.x < NR_N_STAMPS) nr_stamp_acc[threadIdx.x] = 0;               \
+    __syncthreads();                                                            \
+  } while (0)
+#define NR_STAMP_FLUSH()                                                        \
+  do {                                                                          \
+    __syncthreads();                                                            \
+    if (P.stamps && threadIdx.x < NR_N_STAMPS)                                  \
+      atomicAdd((unsigned long long*)&P.stamps[threadIdx.x], nr_stamp_acc[threadIdx.x]); \
   } while (0)
 #else
 #define NR_STAMP(slot) \
   do {                 \
+  } while (0)
+#define NR_STAMP_INIT() \
+  do {                  \
+  } while (0)
+#define NR_STAMP_FLUSH() \
+  do {                   \
   } while (0)
 #endif
 
@@ -575,7 +676,71 @@ __device__ __forceinline__ void profile_contrib(const ProfileParams& P, int k, i
       P.sp_out[(int64_t)m * S + r] = sgn * s / sigma;
     }
   }
-  __syncthreads();
+  nr_sync<NW>();
+}
+
+// The per-node sums of the dual contributions for one wave (S <= 112): the
+// Gram's operand pattern -- lane (i16, kk) reads samples 16 I + i16 (I < 7)
+// of nodes c0 + 4 kk + q, 28 loads per 16-node step, the next step's in
+// flight -- then x_c . u, the column sum and the sum of squares per node,
+// reduced over the 16 sample lanes (rg_row_reduce leaves node c0 + 4 kk + r,
+// r = 2 b3 + b2, in the lanes with lane & 3 == 0). Into L.gv, L.colm (mean)
+// and L.q.
+__device__ __forceinline__ void contrib_dual_sums_wave(const LzLds& L, const double* __restrict__ X, int S, int k,
+                                                       const double* u) {
+  constexpr int NB = 7;
+  const int lane = threadIdx.x & 63;
+  const int i16 = lane & 15, kk = lane >> 4;
+  double ul[NB];
+#pragma unroll
+  for (int I = 0; I < NB; ++I) ul[I] = 16 * I + i16 < S ? u[16 * I + i16] : 0.0;
+  // range-checked buffer loads (out of range reads 0): no branch, so only
+  // this step's loads are waited for (the engine keeps X under 2 GB here)
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
+  auto ld = [&](int c0, double (&v)[NB][4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + 4 * kk + q;
+      const int base = c < k ? (int)L.idx[c] * S : 0;
+#pragma unroll
+      for (int I = 0; I < NB; ++I) {
+        const int s = 16 * I + i16;
+        const int vo = c < k && s < S ? (base + s) * 8 : (int)0x80000000;
+        v[I][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, 0, 0));
+      }
+    }
+  };
+  const int rg = ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+  double cur[NB][4], nxt[NB][4];
+  ld(0, cur);
+  for (int c0 = 0; c0 < k; c0 += 16) {
+    if (c0 + 16 < k) ld(c0 + 16, nxt);
+    double a[4], b[4], q2[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = 0.0;
+      b[q] = 0.0;
+      q2[q] = 0.0;
+#pragma unroll
+      for (int I = 0; I < NB; ++I) {
+        const double x = cur[I][q];
+        a[q] = fma(x, ul[I], a[q]);
+        b[q] += x;
+        q2[q] = fma(x, x, q2[q]);
+      }
+    }
+    const double sa = rg_row_reduce(a, lane), sb = rg_row_reduce(b, lane), sq = rg_row_reduce(q2, lane);
+    const int c = c0 + 4 * kk + rg;
+    if ((lane & 3) == 0 && c < k) {
+      L.gv[c] = sa;
+      L.colm[c] = sb / (double)S;
+      L.q[c] = sq;
+    }
+#pragma unroll
+    for (int I = 0; I < NB; ++I)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[I][q] = nxt[I][q];
+  }
 }
 
 // Node contributions when Lanczos ran on the dual Gram (k > S): L.vv holds u
@@ -595,6 +760,9 @@ __device__ __forceinline__ void profile_contrib_dual(const ProfileParams& P, int
   // flight: the column loads of 8 nodes are issued before any is reduced (the
   // pass was one dependent global round trip per node: 14% of a C2 item)
   const int g16 = lane >> 4, l16 = lane & 15;
+  if constexpr (NW == 1) {
+    contrib_dual_sums_wave(L, X, S, k, u);
+  } else
   for (int c0 = 8 * wave; c0 < k; c0 += 8 * NW) {
     double a[2] = {0.0, 0.0}, b[2] = {0.0, 0.0}, q[2] = {0.0, 0.0};
 #pragma unroll
@@ -642,7 +810,7 @@ __device__ __forceinline__ void profile_contrib_dual(const ProfileParams& P, int
   }
   if (P.sp_out)
     for (int s = tid; s < S; s += BS) P.sp_out[(int64_t)m * S + s] = sgn * u[s];
-  __syncthreads();
+  nr_sync<NW>();
 }
 
 // svd_econ refuses non-finite input -> all-NaN summary (src/netStats.cpp:229-235).
@@ -652,7 +820,7 @@ __device__ __forceinline__ void profile_nonfinite(const ProfileParams& P, int k,
   for (int c = threadIdx.x; c < k; c += BS) L.w[c] = nr_nan();
   if (P.sp_out)
     for (int r = threadIdx.x; r < S; r += BS) P.sp_out[(int64_t)m * S + r] = nr_nan();
-  __syncthreads();
+  nr_sync<NW>();
 }
 
 // ModuleCoherence (src/netStats.cpp:293-305), Correlation / SignAwareMean
@@ -703,7 +871,7 @@ __device__ __forceinline__ void profile_stats(const ProfileParams& P, int k, int
     }
     if (P.coh_out) P.coh_out[m] = stat_coh;
   }
-  __syncthreads();
+  nr_sync<NW>();
 }
 
 // Next item from the persistent queue: (module m, local permutation, CSR
@@ -715,9 +883,9 @@ __device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x;
   if (tid == 0) flags[0] = atomicAdd(P.queue, 1);
-  __syncthreads();
+  nr_sync<NW>();
   const int item = flags[0];
-  __syncthreads();
+  nr_sync<NW>();
   if (item >= P.n_items) return false;
   int64_t mslot;
   const int T = P.order_tail;
@@ -742,7 +910,7 @@ __device__ __forceinline__ bool next_item(const ProfileParams& P, const LzLds& L
   if (idx_used) *idx_used = dst;
   for (int c = tid; c < k; c += BS) dst[c] = node_index(P.src, key, p_local, off + c);
   if (tid == 0) flags[1] = 0;
-  __syncthreads();
+  nr_sync<NW>();
   return true;
 }
 // Weighted-degree fixed-point helpers (the cancellation model of kernels.hip,

@@ -339,13 +339,31 @@ int profile_order_tail(int slots, const std::vector<int32_t>& k_sorted, int firs
   return (top > budget && mix <= budget) ? (int)t : 0;
 }
 
-int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, ProfilePlan* plan) {
+int plan_profile(nr_ctx* ctx, int64_t n_items, int k_max, int n_samples, ProfilePlan* plan, int64_t data_doubles) {
   int dev_cu = 256;
   (void)hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
   int variant = 2;
   // the dual (S x S) Gram of modules with k > S: the Gram side is min(k, S),
   // and so is every Lanczos dimension (basis columns of that length)
   plan->k_gram = std::min(k_max, n_samples);
+  // (its buffer loads take 32-bit byte offsets into the data block)
+  if (plan->k_gram <= nr::kWaveDim && data_doubles * 8 < ((int64_t)1 << 31)) {
+    // the wave class (kernels.h): one wave per item, the Gram in its
+    // registers; the slot's scratch holds the Lanczos basis, and the per-node
+    // arrays of modules longer than the LDS vectors
+    plan->variant = 7;
+    plan->m = nr::kWaveVec;
+    plan->kvec = nr::kWaveVec;
+    plan->big = k_max > nr::kWaveVec;
+    plan->per_cu = nr::profile_wave_per_cu();
+    plan->slots = (int)std::max<int64_t>(1, std::min<int64_t>(n_items, (int64_t)dev_cu * plan->per_cu));
+    plan->gram_doubles = 0;
+    plan->basis_doubles = (int64_t)plan->k_gram * nr::kWaveVec;
+    plan->stride = plan->basis_doubles + (plan->big ? 5 * (int64_t)k_max : 0);
+    plan->stride = (plan->stride + 31) / 32 * 32;
+    plan->g32_off = 0;
+    return NR_OK;
+  }
   if (plan->k_gram <= nr::kSmallDim) {
     // the small class (kernels.h): several small-workgroup items per CU;
     // modules longer than its LDS vectors keep their per-node arrays in the
@@ -481,7 +499,7 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
   int fuse_kind[2] = {0, 0};  // ProfileParams::fused
   for (int i = 0; i < ns; ++i) {
     const int rc = plan_profile(ctx, (int64_t)seg[i].count * n_perm, k_sorted[seg[i].first], (int)pp.n_samples,
-                                &seg[i].plan);
+                                &seg[i].plan, pp.ones_off + 2 * pp.n_samples);
     if (rc) return rc;
     // Gram table: the packed class (compile-time layout, no dual items) takes
     // its network statistics and Gram from the table's gathers, on the table
@@ -847,7 +865,7 @@ bool table_wanted(nr_ctx* ctx) {
     if ((double)n * (double)n * 56.0 > 0.6 * (double)total) return false;
   }
   ProfilePlan plan;
-  if (plan_profile(ctx, 1, packed_max, (int)S, &plan) != NR_OK) return false;
+  if (plan_profile(ctx, 1, packed_max, (int)S, &plan, (int64_t)n * S + 2 * (int64_t)S) != NR_OK) return false;
   return plan.variant == 2 &&
          nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
 }

@@ -19,6 +19,11 @@ constexpr int NR_N_STAMPS = 16;
 // longer than kSmallDim in the slot's scratch.
 constexpr int kSmallDim = 112;
 constexpr int kSmallWaves = 2;  // (one wave per item measured slower: profiles/r03/small_class/)
+// The wave class (round 5, variant 7): Lanczos dimension at most kWaveDim, one
+// wave per item with the item's whole Gram in its registers (kernels.hip).
+constexpr int kWaveBlocks = 7;                // 16-row blocks of the Gram's side (<= 112)
+constexpr int kWaveVec = 16 * kWaveBlocks;     // LDS vector length and Lanczos basis columns
+constexpr int kWaveDim = kWaveVec - 1;         // the side is the dimension plus the ones column
 
 // Where the test column of module node c comes from.
 struct IndexSource {
@@ -187,8 +192,12 @@ hipError_t launch_widen_pairs(const double2* in, const double* gram, double2* ou
 // the small class (variant 5): its LDS bytes per workgroup and workgroups per CU
 size_t profile_small_lds();
 int profile_small_per_cu();
+// the wave class (variant 7): its LDS bytes per workgroup and workgroups per CU
+size_t profile_wave_lds();
+int profile_wave_per_cu();
 // variant 0 full Gram, 2 packed Gram, 4 full Gram with the partials in scratch,
-// 5 the small class, 6 full Gram with the partials and every vector in scratch
+// 5 the small class, 6 full Gram with the partials and every vector in scratch,
+// 7 the wave class (register-resident Gram)
 hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int wg_per_cu,
                           hipStream_t st);
 hipError_t launch_interleave(const double* corr, const double* net, double2* out, int64_t n_elem,

@@ -723,7 +723,7 @@ __device__ __forceinline__ double reorthogonalise_cgs(const double* __restrict__
       for (int t = 0; t < 4; ++t) s[t] += __shfl_xor(s[t], o, 64);
     if (lane < 4 && i0 + lane < n) h[i0 + lane] = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
   }
-  __syncthreads();
+  nr_sync<NW>();
   double nrm[1] = {0.0};
   for (int c = threadIdx.x; c < k; c += NW * 64) {
     double acc = 0.0;
@@ -1479,6 +1479,77 @@ __device__ __forceinline__ double reorthogonalise_bf(const double* __restrict__ 
 
 
 
+// One-wave Lanczos helpers (the wave class): the basis Q (column-major
+// k x n, k <= 128) lives in the slot's global scratch, and a single wave has
+// no other waves to hide a load's latency behind, so each pass keeps 16 basis
+// vectors' loads (both rows of a lane: c = lane, lane + 64) in flight.
+//
+// Classical Gram-Schmidt of w against q_0..q_{n-1} in ONE pass over the
+// basis: h_i = q_i . w for a burst of 16 vectors (transpose-reduce over the
+// lanes, published through h in LDS), and their share of Q h subtracted from
+// the same registers (CGS: every h_i comes from the original w). Returns |w|^2.
+__device__ __forceinline__ double reorthogonalise_wave(const double* __restrict__ Q, int k, int n, double* w,
+                                                       double* h) {
+  const int lane = threadIdx.x & 63;
+  const bool r0 = lane < k, r1 = lane + 64 < k;
+  const double w0 = r0 ? w[lane] : 0.0, w1 = r1 ? w[lane + 64] : 0.0;
+  double d0 = 0.0, d1 = 0.0;
+  for (int i0 = 0; i0 < n; i0 += 16) {
+    double a[16], b[16], p[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int i = i0 + t;
+      a[t] = i < n && r0 ? Q[(int64_t)i * k + lane] : 0.0;
+      b[t] = i < n && r1 ? Q[(int64_t)i * k + lane + 64] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) p[t] = fma(b[t], w1, a[t] * w0);
+    const double v = nr_transpose_reduce16(p, lane);
+    if ((lane & 3) == 0) {
+      const int t = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+      if (i0 + t < n) h[i0 + t] = v;
+    }
+    nr_sync<1>();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const double ht = i0 + t < n ? h[i0 + t] : 0.0;
+      d0 = fma(ht, a[t], d0);
+      d1 = fma(ht, b[t], d1);
+    }
+  }
+  const double z0 = w0 - d0, z1 = w1 - d1;
+  if (r0) w[lane] = z0;
+  if (r1) w[lane + 64] = z1;
+  return nr_wave_sum(z0 * z0 + z1 * z1);
+}
+
+// v = Q y over the first n basis vectors (rows c = lane, lane + 64 < k), the
+// terms in basis order as the general loop.
+__device__ __forceinline__ void ritz_vector_wave(const double* __restrict__ Q, int k, int n, const double* y,
+                                                 double* v) {
+  const int lane = threadIdx.x & 63;
+  const bool r0 = lane < k, r1 = lane + 64 < k;
+  double s0 = 0.0, s1 = 0.0;
+  for (int i0 = 0; i0 < n; i0 += 16) {
+    double a[16], b[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int i = i0 + t;
+      a[t] = i < n && r0 ? Q[(int64_t)i * k + lane] : 0.0;
+      b[t] = i < n && r1 ? Q[(int64_t)i * k + lane + 64] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const double yt = i0 + t < n ? y[i0 + t] : 0.0;
+      s0 = fma(yt, a[t], s0);
+      s1 = fma(yt, b[t], s1);
+    }
+  }
+  if (r0) v[lane] = s0;
+  if (r1) v[lane + 64] = s1;
+  nr_sync<1>();
+}
+
 // Lanczos for the top eigenpair of the k x k operator mv (mv(x, out, y)
 // writes out = G x for rows < k and returns y . out; x is zero beyond k):
 // three-term update, partial reorthogonalisation by the omega recurrence
@@ -1530,7 +1601,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     for (int c = tid; c < k; c += BS) q[c] *= inv;
   }
   if (tid == 0) s_done = 0;
-  __syncthreads();
+  nr_sync<NW>();
   int nsteps = 0;
   double beta_prev = 0.0;
   // First convergence check at step 16; later checks where the residual's
@@ -1568,14 +1639,17 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       const double mx = omega_update(alpha, beta, j, alpha0, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
       if (lane == 0) s_reorth = force_next || mx > sqrt_eps;
     }
-    __syncthreads();
+    nr_sync<NW>();
     NR_STAMP(4);  // Lanczos: three-term step + omega recurrence
     if (s_reorth) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
-      nb = BF ? reorthogonalise_bf<NW>(Q, k, j + 1, w, h, twork, 5 * mmax, red)  // twork idle until the next check
-              : reorthogonalise_cgs<NW>(Q, k, j + 1, w, h, red);
+      if constexpr (NW == 1)
+        nb = reorthogonalise_wave(Q, k, j + 1, w, h);
+      else
+        nb = BF ? reorthogonalise_bf<NW>(Q, k, j + 1, w, h, twork, 5 * mmax, red)  // twork idle until the next check
+                : reorthogonalise_cgs<NW>(Q, k, j + 1, w, h, red);
       if (BF) {  // twork is the packed matvec's partial array: zero again
         for (int i = tid; i < 5 * mmax; i += BS) twork[i] = 0.0;
-        __syncthreads();
+        nr_sync<NW>();
       }
       alpha_j += h[j];
       if (wave == 0) {
@@ -1603,12 +1677,12 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       }
     }
     beta_prev = beta_j;
-    __syncthreads();
+    nr_sync<NW>();
     NR_STAMP(6);  // Lanczos: q update + barrier
     const bool last = (j + 1 == mcap);
     if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
       if (wave == 0) {
-        const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane, hint_theta, hint_r);
+        const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane, hint_theta, hint_r, h, ty);  // h, ty idle here
         const double resid = tri_top_resid(alpha, beta, j + 1, theta, beta_j, ty, lane);
         hint_theta = theta;
         hint_r = resid;
@@ -1639,7 +1713,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
           s_next_check = min(j + 1 + step, mcap);
         }
       }
-      __syncthreads();
+      nr_sync<NW>();
       if (s_done) break;
       next_check = s_next_check;
       if (relax) *relax = flags[5] != 0;
@@ -1661,12 +1735,21 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   double nv[1] = {0.0};
   const double theta_f = gv_out ? L.h[0] : 0.0;
   const double ym = gv_out ? ty[nsteps - 1] : 0.0;
-  for (int c = tid; c < k; c += BS) {
-    double s = 0.0;
-    for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
-    L.vv[c] = s;
-    if (gv_out) L.gv[c] = theta_f * s + ym * w[c];
-    nv[0] += s * s;
+  if constexpr (NW == 1) {  // one wave: 16 basis vectors' loads in flight per burst (ritz_vector_wave)
+    ritz_vector_wave(Q, k, nsteps, ty, L.vv);
+    for (int c = tid; c < k; c += BS) {
+      const double s = L.vv[c];
+      if (gv_out) L.gv[c] = theta_f * s + ym * w[c];
+      nv[0] += s * s;
+    }
+  } else {
+    for (int c = tid; c < k; c += BS) {
+      double s = 0.0;
+      for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
+      L.vv[c] = s;
+      if (gv_out) L.gv[c] = theta_f * s + ym * w[c];
+      nv[0] += s * s;
+    }
   }
   if (BF)  // twork (the packed matvec's partials) held the tridiagonal LU: zero again
     for (int i = tid; i < 5 * mmax; i += BS) twork[i] = 0.0;
@@ -1678,7 +1761,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       if (gv_out) L.gv[c] *= inv;
     }
   }
-  __syncthreads();
+  nr_sync<NW>();
   NR_STAMP(10);  // Ritz vector
 }
 
@@ -1702,6 +1785,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
 template <int NW, bool PACKED, int KB, int MB = 0, bool TABLE = false, bool G64 = false>
 __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   constexpr int BS = NW * 64;
+  NR_STAMP_INIT();
   uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_flags[8];
@@ -1841,6 +1925,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     profile_stats<NW>(P, k, m, off, p_local, Li);
     NR_STAMP(5);  // Ritz vector, contributions, statistics
   }
+  NR_STAMP_FLUSH();
 }
 
 __global__ void __launch_bounds__(NR_BS, 3)
@@ -1882,6 +1967,348 @@ template <int NW>
 __global__ void __launch_bounds__(NW * 64, kSmallOcc)
 module_profile_small_kernel(ProfileParams P) {
   profile_body<NW, true, kSmallDim, kSmallDim>(P);
+}
+
+// ---------------------------------------------------------------------------
+// The wave class (round 5): Lanczos dimension n = min(k, S) <= kWaveDim, one
+// wave per item, and the item's whole Gram [X 1]^T [X 1] (side n + 1 <= 112,
+// seven 16-row blocks) kept in the wave's registers as its 28 lower 16 x 16
+// MFMA accumulator tiles (tile (I, J), I >= J, at I (I + 1) / 2 + J; a
+// diagonal tile holds both of its triangles). The Gram is never written to
+// memory, and every Lanczos matvec reads it from registers: the small class
+// streamed a ~41 KB packed Gram per matvec from the cache hierarchy, about 40
+// times per item, latency-bound (57% of a C2 item, profiles/r04/stamps/
+// stamps_C2.txt). Lane (i16, kk) = (lane & 15, lane >> 4) holds
+// G[16 I + kk + 4 r][16 J + i16], r = 0..3 (f64 MFMA C/D map). 224 registers
+// of Gram put one wave on each SIMD: four items per CU, each on its own
+// matrix core.
+// ---------------------------------------------------------------------------
+constexpr int kWaveTiles = kWaveBlocks * (kWaveBlocks + 1) / 2;
+static_assert(kWaveDim + 1 <= kWaveVec, "the wave class's Gram side must fit its tiles");
+
+__device__ __forceinline__ constexpr int wave_tile(int I, int J) { return I * (I + 1) / 2 + J; }
+
+// A Gram value for the VALU. (Reading the tiles through an inline-asm AGPR
+// operand kept them out of VGPRs too, but hides the MFMA -> read hazard from
+// the compiler; with one MFMA site the allocator keeps them in AGPRs itself,
+// 64 B/lane of spill outside the matvec.)
+__device__ __forceinline__ double tile_val(const nr_f64x4& t, int r) { return t[r]; }
+
+// The Gram on the matrix cores, straight into the tiles. Primal (k <= S): the
+// vectors are the module's columns (block position c < k: column idx[c];
+// c == k: the data block's ones column; beyond: its zero column), contracted
+// over the S samples, each lane feeding 4 consecutive samples of its column
+// per 16-sample step (two 16-byte loads), as gram_mfma. Dual (k > S): the
+// vectors are the samples (position s < S: row s of X; s == S: the ones row;
+// beyond: zero), contracted over the k module nodes, each lane feeding nodes
+// c0 + 4 kk + q of a 16-node step (16 lanes read 16 consecutive samples of a
+// column), as gram_mfma_dual. One operand register per block serves as A for
+// the block's tile row and as B for its tile column; the next step's operands
+// are in flight during this step's MFMAs. One MFMA site for both shapes (two
+// sites put the tiles in VGPRs and spilled). nb: blocks of the side n + 1.
+__device__ __forceinline__ void gram_wave(const double* __restrict__ X, int S, const uint32_t* idx, int k,
+                                          int64_t ones_off, int nb, bool dual, nr_f64x4 (&T)[kWaveTiles]) {
+  const int lane = threadIdx.x & 63;
+  const int i16 = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < kWaveTiles; ++t) T[t] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+  // Every operand is a range-checked buffer load (an out-of-range offset
+  // reads 0, no branch), so the compiler counts the loads in flight exactly
+  // and waits for this step's operands only, not the next step's too.
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((ones_off + 2 * (int64_t)S) * 8),
+                                                      0x00020000);
+  constexpr int OOR = (int)0x80000000;
+  int col[kWaveBlocks];  // primal: the lane's column of each block (element offset)
+#pragma unroll
+  for (int I = 0; I < kWaveBlocks; ++I) {
+    const int c = 16 * I + i16;
+    col[I] = c < k ? (int)idx[c] * S : (int)(c == k ? ones_off : ones_off + S);
+  }
+  auto ld = [&](int st, double (&v)[kWaveBlocks][4]) {
+    if (!dual) {
+      const int s0 = 16 * st + 4 * kk;
+#pragma unroll
+      for (int I = 0; I < kWaveBlocks; ++I)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int vo = I < nb && s0 + q < S ? (col[I] + s0 + q) * 8 : OOR;
+          v[I][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, 0, 0));
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 16 * st + 4 * kk + q;
+        const int base = c < k ? (int)idx[c] * S : 0;
+#pragma unroll
+        for (int I = 0; I < kWaveBlocks; ++I) {
+          const int s = 16 * I + i16;
+          const int vo = I < nb && c < k && s < S ? (base + s) * 8 : OOR;
+          const double x = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, 0, 0));
+          v[I][q] = s == S && c < k ? 1.0 : x;  // the ones row
+        }
+      }
+    }
+  };
+  const int nsteps = dual ? (k + 15) / 16 : (S + 15) / 16;
+  double cur[kWaveBlocks][4], nxt[kWaveBlocks][4];
+  ld(0, cur);
+  for (int st = 0; st < nsteps; ++st) {
+    if (st + 1 < nsteps) ld(st + 1, nxt);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int I = 0; I < kWaveBlocks; ++I) {
+        if (I >= nb) break;
+#pragma unroll
+        for (int J = 0; J <= I; ++J)
+          T[wave_tile(I, J)] =
+              __builtin_amdgcn_mfma_f64_16x16x4f64(cur[I][q], cur[J][q], T[wave_tile(I, J)], 0, 0, 0);
+      }
+#pragma unroll
+    for (int I = 0; I < kWaveBlocks; ++I)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[I][q] = nxt[I][q];
+  }
+}
+
+__device__ __forceinline__ double sel4(const nr_f64x4& t, int r) {
+  const double a = tile_val(t, 0), b = tile_val(t, 1), c = tile_val(t, 2), d = tile_val(t, 3);
+  return r == 0 ? a : (r == 1 ? b : (r == 2 ? c : d));
+}
+
+// What the rest of the item needs from the tiles: the diagonal G_cc (c < n,
+// into dg), the non-finite flag (a non-finite diagonal entry, as the other
+// Gram schemes), the column means (primal: row k of G is the column sums),
+// and the per-lane part of 1'G1 over the X block (primal: the sum of G over
+// c, c' < k; dual: |X 1|^2 from the ones row).
+__device__ __forceinline__ void gram_wave_epilogue(const nr_f64x4 (&T)[kWaveTiles], int nb, int n, int k, int S,
+                                                   bool dual, double* dg, double* colm, double& g1, int& bad) {
+  const int lane = threadIdx.x & 63;
+  const int i16 = lane & 15, kk = lane >> 4;
+  // the lane's entry of a diagonal tile's diagonal: row kk + 4 r == column i16
+  const bool has_diag = i16 >= kk && ((i16 - kk) & 3) == 0;
+  const int rd = (i16 - kk) >> 2;
+  // the ones row (index n: k primal, S dual): tile row n >> 4, the lanes whose
+  // row kk + 4 r is n & 15
+  const int In = n >> 4, rn = (n & 15) - kk;
+  const bool has_ones = rn >= 0 && (rn & 3) == 0;
+#pragma unroll
+  for (int I = 0; I < kWaveBlocks; ++I) {
+    if (I >= nb) break;
+    if (has_diag && 16 * I + i16 < n) {
+      const double val = sel4(T[wave_tile(I, I)], rd);
+      dg[16 * I + i16] = val;
+      bad |= (int)!isfinite(val);
+    }
+    if (I == In && has_ones) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int gj = 16 * J + i16;
+        const double val = sel4(T[wave_tile(I, J)], rn >> 2);
+        if (gj < n) {
+          if (dual)
+            g1 += val * val;
+          else
+            colm[gj] = val / (double)S;
+        }
+      }
+    }
+    if (!dual) {  // 1'G1 over the k x k block: tiles below the diagonal count twice
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const double wgt = I == J ? 1.0 : 2.0;
+        const int gj = 16 * J + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = 16 * I + kk + 4 * r;
+          g1 += (gi < k && gj < k) ? wgt * tile_val(T[wave_tile(I, J)], r) : 0.0;
+        }
+      }
+    }
+  }
+}
+
+// out = G x over the leading n x n block (x zero at n and beyond; rows >= n
+// not written), from the registers. Lower tiles (I >= J, diagonal tiles
+// whole): lane-local sums over the tile's columns, then over the 16 column
+// lanes (rg_row_reduce) into ylo; mirrored part of the tiles below the
+// diagonal (I > J): lane-local sums over the tile rows, then over the four
+// row groups (two permlane swaps) into yup; out = ylo + yup. A fixed order
+// throughout: bitwise reproducible. Returns sum_r y_r out_r if y (every lane).
+// SQ: out_r = sum_c G_rc^2 over c < n instead (start column norms; x unused).
+template <bool SQ>
+__device__ __forceinline__ double wave_matvec(const nr_f64x4 (&T)[kWaveTiles], int nb, int n, const double* x,
+                                              double* out, const double* y, double* ylo, double* yup) {
+  const int lane = threadIdx.x & 63;
+  const int i16 = lane & 15, kk = lane >> 4;
+  double xc[kWaveBlocks], au[kWaveBlocks];
+#pragma unroll
+  for (int I = 0; I < kWaveBlocks; ++I) {
+    au[I] = 0.0;
+    xc[I] = 0.0;
+    if (I < nb) xc[I] = SQ ? (16 * I + i16 < n ? 1.0 : 0.0) : x[16 * I + i16];
+  }
+  const int rg = 4 * (((lane >> 3) & 1) * 2 + ((lane >> 2) & 1));  // row offset of rg_row_reduce's group
+  // one pass over the tiles, each value read once: tile row I's lower sums
+  // (reduced and stored when the row is done) and, below the diagonal, the
+  // mirrored sums of the tile columns J < I
+#pragma unroll
+  for (int I = 0; I < kWaveBlocks; ++I) {
+    if (I >= nb) break;
+    double xri[4], a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xri[r] = SQ ? (16 * I + kk + 4 * r < n ? 1.0 : 0.0) : x[16 * I + kk + 4 * r];
+#pragma unroll
+    for (int J = 0; J <= I; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double g = tile_val(T[wave_tile(I, J)], r);
+        const double gg = SQ ? g * g : g;
+        a[r] = fma(gg, xc[J], a[r]);
+        if (J < I) au[J] = fma(gg, xri[r], au[J]);
+      }
+    const double v = rg_row_reduce(a, lane);
+    if ((lane & 3) == 0) ylo[16 * I + kk + rg] = v;
+  }
+#pragma unroll
+  for (int J = 0; J < kWaveBlocks; ++J) {
+    if (J >= nb) break;
+    double a = nr_swap16_sum(au[J], au[J]);
+    a = nr_swap32_sum(a, a);
+    if (kk == 0) yup[16 * J + i16] = a;
+  }
+  nr_sync<1>();  // one wave: orders the LDS writes above before the reads below
+  double d = 0.0;
+  for (int c = lane; c < n; c += 64) {
+    const double s = ylo[c] + yup[c];
+    out[c] = s;
+    if (y) d += y[c] * s;
+  }
+  return y ? nr_wave_sum(d) : 0.0;
+}
+
+// Lanczos start vector q = G e_c* for the column c* of largest norm (ties to
+// the smaller index), as start_column; norms from the fp64 tiles. Returns
+// false (q untouched) if every column is zero. e: kWaveVec doubles of LDS.
+__device__ __forceinline__ bool wave_start_column(const nr_f64x4 (&T)[kWaveTiles], int nb, int n, double* q,
+                                                  double* cn, double* e, double* ylo, double* yup) {
+  const int lane = threadIdx.x & 63;
+  wave_matvec<true>(T, nb, n, nullptr, cn, nullptr, ylo, yup);
+  nr_sync<1>();
+  double best = -1.0;
+  int bi = 0x7fffffff;
+  for (int r = lane; r < n; r += 64) {
+    const double v = cn[r];
+    if (v > best) {
+      best = v;
+      bi = r;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) {
+      best = ov;
+      bi = oi;
+    }
+  }
+  const bool ok = best > 0.0 && bi < n;
+  if (ok) {
+    for (int c = lane; c < kWaveVec; c += 64) e[c] = c == bi ? 1.0 : 0.0;
+    nr_sync<1>();
+    wave_matvec<false>(T, nb, n, e, q, nullptr, ylo, yup);  // exact: one nonzero per row sum
+  }
+  nr_sync<1>();
+  return ok;
+}
+
+// LDS of the wave kernel: carve_lds<1> with vectors of kWaveVec, a basis of
+// kWaveVec columns, and three extra vectors (ylo, yup, the Gram diagonal).
+size_t profile_wave_lds() {
+  constexpr size_t kv = kWaveVec, mb = kWaveVec;
+  return sizeof(double) * (8 + 6 * kv + 3 * kv + 4 * mb + 5 * mb + 3 * (mb + 1)) + sizeof(uint32_t) * kv;
+}
+
+int profile_wave_per_cu() {
+  const int by_lds = (int)((160 * 1024) / profile_wave_lds());
+  return by_lds < 4 ? by_lds : 4;  // one wave per SIMD (the Gram's registers)
+}
+
+__global__ void __launch_bounds__(64, 1)
+module_profile_wave_kernel(ProfileParams P) {
+  constexpr int KB = kWaveVec, MB = kWaveVec;
+  NR_STAMP_INIT();
+  uint64_t t_mark = P.stamps && threadIdx.x == 0 ? nr_clock() : 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_flags[8];
+  const int lane = threadIdx.x;
+  const int S = (int)P.n_samples;
+  // the slot's scratch: the Lanczos basis (no Gram in memory), then the
+  // per-node arrays and index set of modules longer than the LDS vectors
+  double* Q = P.scratch + (int64_t)blockIdx.x * P.scratch_stride;
+  double* ext;
+  const LzLds L = carve_lds<1>(smem, KB, MB, 3 * KB, &ext);
+  double* ylo = ext;
+  double* yup = ext + KB;
+  double* dg = ext + 2 * KB;
+  double* gnode = Q + P.basis_doubles;
+  const double* __restrict__ X = P.data;
+  int m, k;
+  int64_t p_local, off;
+  uint32_t* idx_p = L.idx;
+  while (next_item<1>(P, L, s_flags, m, p_local, off, k, KB,
+                      reinterpret_cast<uint32_t*>(gnode + 4 * (int64_t)P.k_max), &idx_p)) {
+    NR_STAMP(0);
+    LzLds Li = L;
+    Li.idx = idx_p;
+    if (k > KB) {
+      Li.gv = gnode;
+      Li.colm = gnode + P.k_max;
+      Li.q = gnode + 2 * (int64_t)P.k_max;
+      Li.w = gnode + 3 * (int64_t)P.k_max;
+    }
+    const bool dual = k > S;
+    const int n = dual ? S : k;  // Lanczos dimension
+    const int nb = (n + 16) / 16;  // blocks of the Gram's side n + 1
+    // the matvec operands read x up to the last block: zero beyond n (the
+    // previous item's per-node arrays may have left values there)
+    for (int c = n + lane; c < KB; c += 64) {
+      L.q[c] = 0.0;
+      L.vv[c] = 0.0;
+    }
+    nr_f64x4 T[kWaveTiles];
+    gram_wave(X, S, Li.idx, k, P.ones_off, nb, dual, T);
+    double g1 = 0.0;
+    int bad = 0;
+    gram_wave_epilogue(T, nb, n, k, S, dual, dg, L.colm, g1, bad);
+    g1 = nr_wave_sum(g1);
+    bool nonfinite = __ballot(bad != 0) != 0;
+#ifdef NR_GRAM_ONLY
+    nonfinite = true;  // diagnostic build only: the Gram phase alone (see profile_body)
+#endif
+    nr_sync<1>();  // dg, colm published; the zeroed vector tails too
+    NR_STAMP(1);
+    if (!nonfinite) {
+      auto mv = [&](const double* x, double* out, const double* y) -> double {
+        return wave_matvec<false>(T, nb, n, x, out, y, ylo, yup);
+      };
+      const bool q_given = wave_start_column(T, nb, n, L.q, L.w, L.vv, ylo, yup);
+      NR_STAMP(8);
+      lanczos_ritz<1, false>(P, n, L, s_flags, Q, mv, t_mark, nullptr, q_given, !dual);
+      if (dual) {
+        profile_contrib_dual<1>(P, k, m, Li, X, S, g1);
+      } else {
+        profile_contrib<1>(P, k, m, L, X, S, g1, mv, [&](int c) { return dg[c]; }, true);
+      }
+      NR_STAMP(11);
+    } else {
+      profile_nonfinite<1>(P, k, m, S, Li);
+    }
+    profile_stats<1>(P, k, m, off, p_local, Li);
+    NR_STAMP(5);
+  }
+  NR_STAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -2209,6 +2636,10 @@ hipError_t launch_profile(const ProfileParams& P, int n_slots, int variant, int 
       hipLaunchKernelGGL(module_profile_big_kernel, g, b4, lds, st, P);
     else
       hipLaunchKernelGGL((module_profile_packed4_kernel<0, 2>), g, b4, lds, st, P);
+    return hipGetLastError();
+  }
+  if (variant == 7) {
+    hipLaunchKernelGGL(module_profile_wave_kernel, g, dim3(64), profile_wave_lds(), st, P);
     return hipGetLastError();
   }
   if (variant == 5) {

@@ -1,0 +1,14 @@
+# Round 5: wave class + leaner Sturm passes + one-wave block sums: tests, A/B, stamps, C2 bench.
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+D=gpurun_out/r5wave8
+mkdir -p $D
+( while sleep 50; do date >> $D/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 300 python -u -m pytest tests/test_abi_driver.py tests/test_gpu_small.py tests/test_gpu_dual.py tests/test_gpu_configs.py -m gpu -x -v --timeout 200 --timeout-method thread > $D/pytest_small.txt 2>&1
+timeout -k 10 300 python -u tools/probes/profile_ab.py 100 30 300 20 small=netrep_amd/_lib/ab/base.so wave=- > $D/ab_C2.txt 2>&1
+timeout -k 10 300 python -u tools/probes/profile_ab.py 100 30 300 20 wave_st=netrep_amd/_lib/diag/wave_stamps.so > $D/stamps_C2.txt 2>&1
+timeout -k 10 300 python -u tools/probes/profile_ab.py 500 30 300 50 base=netrep_amd/_lib/ab/base.so tree=- > $D/ab_C3.txt 2>&1
+timeout -k 10 300 python -u bench.py --config C2 --no-cpu-baseline > $D/C2.json 2> $D/C2.err
