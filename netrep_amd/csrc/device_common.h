@@ -298,6 +298,7 @@ static __device__ __forceinline__ void tri_eigenvector(const double* __restrict_
   double* __restrict__ du2 = work + 3 * n;
   double* __restrict__ swp = work + 4 * n;
   double scale = fabs(theta);
+#pragma unroll 4
   for (int i = 0; i < n; ++i) {
     scale = fmax(scale, fabs(alpha[i]));
     if (i < n - 1) scale = fmax(scale, fabs(beta[i]));
@@ -305,32 +306,25 @@ static __device__ __forceinline__ void tri_eigenvector(const double* __restrict_
   const double floor_piv = 1e-300 + 2.2e-16 * scale;
   double di = alpha[0] - theta;          // current pivot candidate d_i
   double dui = n > 1 ? beta[0] : 0.0;    // current super-diagonal du_i
+  // branch-free steps (selects instead of the two pivoting paths), so the
+  // loop unrolls and the next steps' LDS reads overlap this step's chain
+#pragma unroll 4
   for (int i = 0; i < n - 1; ++i) {
     const double bi = beta[i];                       // sub-diagonal dl_i
     const double dn = alpha[i + 1] - theta;          // d_{i+1} before this step
     const double dun = i < n - 2 ? beta[i + 1] : 0.0;  // du_{i+1} before this step
-    if (fabs(di) >= fabs(bi)) {
-      if (fabs(di) < floor_piv) di = di < 0.0 ? -floor_piv : floor_piv;
-      const double r = 1.0 / di;
-      const double f = bi * r;
-      dl[i] = f;
-      rd[i] = r;
-      du[i] = dui;
-      du2[i] = 0.0;
-      swp[i] = 0.0;
-      di = dn - f * dui;
-      dui = dun;
-    } else {  // row interchange
-      const double r = 1.0 / bi;
-      const double f = di * r;
-      dl[i] = f;
-      rd[i] = r;
-      du[i] = dn;
-      du2[i] = dun;
-      swp[i] = 1.0;
-      di = dui - f * dn;
-      dui = -f * dun;
-    }
+    const bool sw = !(fabs(di) >= fabs(bi));         // row interchange
+    const double dc = fabs(di) < floor_piv ? (di < 0.0 ? -floor_piv : floor_piv) : di;
+    const double r = 1.0 / (sw ? bi : dc);
+    const double f = (sw ? di : bi) * r;
+    dl[i] = f;
+    rd[i] = r;
+    du[i] = sw ? dn : dui;
+    du2[i] = sw ? dun : 0.0;
+    swp[i] = sw ? 1.0 : 0.0;
+    const double ndi = sw ? dui - f * dn : dn - f * dui;
+    dui = sw ? -f * dun : dun;
+    di = ndi;
   }
   if (fabs(di) < floor_piv) di = di < 0.0 ? -floor_piv : floor_piv;
   rd[n - 1] = 1.0 / di;
@@ -338,21 +332,19 @@ static __device__ __forceinline__ void tri_eigenvector(const double* __restrict_
   for (int iter = 0; iter < 2; ++iter) {
     // L solve (the row interchanges applied as the factorisation made them)
     double yi = iter == 0 ? 1.0 : y[0] * sc;
+#pragma unroll 4
     for (int i = 0; i < n - 1; ++i) {
       const double yn = iter == 0 ? 1.0 : y[i + 1] * sc;
-      const double f = dl[i];
-      if (swp[i] == 0.0) {
-        y[i] = yi;
-        yi = yn - f * yi;
-      } else {
-        y[i] = yn;
-        yi = yi - f * yn;
-      }
+      const bool sw = swp[i] != 0.0;
+      const double a = sw ? yn : yi, b = sw ? yi : yn;
+      y[i] = a;
+      yi = b - dl[i] * a;
     }
     // U solve (bandwidth 3)
     double y1 = yi * rd[n - 1], y2 = 0.0;
     y[n - 1] = y1;
     double mx = fabs(y1);
+#pragma unroll 4
     for (int i = n - 2; i >= 0; --i) {
       const double y0 = (y[i] - du[i] * y1 - du2[i] * y2) * rd[i];
       y[i] = y0;
@@ -363,12 +355,14 @@ static __device__ __forceinline__ void tri_eigenvector(const double* __restrict_
     sc = 1.0 / mx;
   }
   double nrm = 0.0;
+#pragma unroll 4
   for (int i = 0; i < n; ++i) {
     const double v = y[i] * sc;
     y[i] = v;
     nrm += v * v;
   }
   const double inv = 1.0 / sqrt(nrm);
+#pragma unroll 4
   for (int i = 0; i < n; ++i) y[i] *= inv;
 }
 

@@ -116,7 +116,13 @@ struct ProfileParams {
 // test column (each column chunk streamed into LDS once, every occurrence of
 // the column reads its rows there) instead of one random gather per pair.
 constexpr int kSweepWaves = 16;                   // waves per (column, chunk) workgroup: one per CU
-constexpr int kSweepLanes = 8;                    // lanes per occurrence (16: 2-5% slower, r05/l8b)
+// Lanes per occurrence: 8 (16: 2-5% slower at C4 / C2, r05/l8b), except where a
+// module exceeds kSweepWideK nodes (C5): 16 lanes halve each
+// occurrence's serial run over its entries, and at C5's 64-permutation
+// launches (~64 occurrences per column) eight-lane batches fill only half of
+// a workgroup's 16 waves (C5 sweep 12.8 ms per 64 permutations at 16 lanes,
+// 16.3 at 8: profiles/r05/final3/C5.json, profiles/r05/sweep16/)
+constexpr int kSweepWideK = 1024;
 constexpr int kSweepMaxChunks = 16;               // chunks per column (n <= 65,535)
 constexpr int kSweepMaxK = 4096;                  // module nodes (LDS of the per-item kernels)
 constexpr int64_t kSweepChunkBytes = 160000;      // LDS per (column, chunk) workgroup

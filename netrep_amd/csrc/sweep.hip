@@ -182,6 +182,34 @@ __device__ __forceinline__ unsigned long long sw_dpp_u64(unsigned long long v) {
   return ((unsigned long long)hi << 32) | lo;
 }
 
+// Sixteen-lane groups (modules beyond kSweepWideK nodes): sums of v[0..16)
+// over the 16 lanes of each row, transposed: afterwards lane gl of the row
+// holds the total of v[gl]. Four DPP exchange levels on lane bits 3..0,
+// halving the values at each (15 exchanges, not 64); fixed order.
+__device__ __forceinline__ double sw_transpose16(const double (&v)[16], int lane) {
+  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+  double a8[8], a4[4], a2[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a8[i] = (b3 ? v[i + 8] : v[i]) + nr_dpp<NR_DPP_ROR8>(b3 ? v[i] : v[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)  // lane ^ 7: the partner's bits 1, 0 differ too; later levels cover them
+    a4[i] = (b2 ? a8[i + 4] : a8[i]) + nr_dpp<NR_DPP_HALF_MIRROR>(b2 ? a8[i] : a8[i + 4]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) a2[i] = (b1 ? a4[i + 2] : a4[i]) + nr_dpp<NR_DPP_XOR2>(b1 ? a4[i] : a4[i + 2]);
+  return (b0 ? a2[1] : a2[0]) + nr_dpp<NR_DPP_XOR1>(b0 ? a2[0] : a2[1]);
+}
+// ... and four exact integer sums: lanes with bits (3, 2) = (i, j) hold the
+// total of v[2i + j].
+__device__ __forceinline__ unsigned long long sw_transpose4_u64(const unsigned long long (&v)[4], int lane) {
+  const bool b3 = lane & 8, b2 = lane & 4;
+  unsigned long long a2[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) a2[i] = (b3 ? v[i + 2] : v[i]) + sw_dpp_u64<NR_DPP_ROR8>(b3 ? v[i] : v[i + 2]);
+  unsigned long long x = (b2 ? a2[1] : a2[0]) + sw_dpp_u64<NR_DPP_HALF_MIRROR>(b2 ? a2[0] : a2[1]);
+  x += sw_dpp_u64<NR_DPP_XOR2>(x);
+  return x + sw_dpp_u64<NR_DPP_XOR1>(x);
+}
+
 // Eight-lane groups: the same exchanges over lane bits 2..0 (mirror within
 // 8, XOR 2, XOR 1), 16 values -> 2 per lane: lane bits (b2 b1 b0) hold the
 // totals of v[8 b2 + 4 b1 + 2 b0] and the next one.
@@ -272,12 +300,13 @@ __device__ __forceinline__ uint32_t sw_range(const SweepParams& P, const SwOcc& 
 // Lane gl's entries gl + 16 (t0 + t) of the occurrence's chunk range: one
 // offset, the steps as immediates. Entries past the range (the next item's,
 // or past the array: 0) are loaded but never used (sw_block skips them).
+template <int L>
 __device__ __forceinline__ void sw_entries(const SwRsrc& R, const SwOcc& q, uint32_t bd, int gl, int t0,
                                            uint32_t (&u)[kSweepPre]) {
-  const uint32_t off = (q.mt.x + (bd & 0xFFFFu) + (uint32_t)gl + (uint32_t)(kSweepLanes * t0)) * 4u;
+  const uint32_t off = (q.mt.x + (bd & 0xFFFFu) + (uint32_t)gl + (uint32_t)(L * t0)) * 4u;
 #pragma unroll
   for (int t = 0; t < kSweepPre; ++t)
-    u[t] = __builtin_amdgcn_raw_buffer_load_b32(R.sorted, off + (uint32_t)(t * kSweepLanes * 4), 0, 0);
+    u[t] = __builtin_amdgcn_raw_buffer_load_b32(R.sorted, off + (uint32_t)(t * L * 4), 0, 0);
 }
 
 // The discovery CorrVector values of the lane's pairs (ii = r > jj, jj),
@@ -330,7 +359,7 @@ __device__ __forceinline__ unsigned long long sw_fx(double v) {
 // it skips the body), the rest is branch-free. FIN: the test correlations and
 // the discovery CorrVector are all finite (no complete-case tests; xv is
 // already 0 off the pairs).
-template <bool X, bool FIN>
+template <bool X, bool FIN, int L>
 __device__ __forceinline__ void sw_block(const void* colv_, int64_t row0, const SwOcc& q, uint32_t bd, int gl,
                                          int t0, const uint32_t (&u)[kSweepPre], const double (&xv)[kSweepPre],
                                          int gj, SwAcc& A) {
@@ -341,7 +370,7 @@ __device__ __forceinline__ void sw_block(const void* colv_, int64_t row0, const 
   const bool same = ((pj ^ (e0 + gl)) & 1) == 0;
 #pragma unroll
   for (int t = 0; t < kSweepPre; ++t) {
-    const int e = e0 + gl + kSweepLanes * (t0 + t);
+    const int e = e0 + gl + L * (t0 + t);
     if (e >= e1) continue;
     const int r = (int)(u[t] & 0xFFFFu);
     const E v = colv[(int64_t)(u[t] >> 16) - row0];
@@ -390,7 +419,7 @@ __device__ __forceinline__ void sw_block(const void* colv_, int64_t row0, const 
 // per (occurrence, chunk), summed in chunk order by sweep_finish_kernel. The
 // next batch's entries and the one after's metadata load while a batch is
 // summed.
-template <bool X, bool FIN>
+template <bool X, bool FIN, int L>
 __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepParams P) {
   using E = typename std::conditional<X, double2, double>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -429,10 +458,10 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
   const int gj = wd_grid_exp(dg);
   if (h == 0 && threadIdx.x == 0) P.dabs[c] = dg;  // for the finish kernel's weighted degrees
   __syncthreads();
-  constexpr int G = 64 / kSweepLanes;  // occurrences per wave batch
+  constexpr int G = 64 / L;  // occurrences per wave batch
   constexpr int32_t stride = G * kSweepWaves;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int grp = lane / kSweepLanes, gl = lane % kSweepLanes;
+  const int grp = lane / L, gl = lane % L;
   SwRsrc R;
   R.meta = sw_rsrc(P.meta, P.n_occ * 32);
   R.bndh = sw_rsrc(P.bndh, P.n_chunks > 2 ? P.n_occ * 4 * P.n_chunks : 0);
@@ -442,7 +471,7 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
   uint32_t uc[kSweepPre];
   int32_t sb = o0 + G * wave;
   sw_fetch<X>(P, R, h, sb + grp, o1, cur);
-  sw_entries(R, cur, sw_range(P, cur, h), gl, 0, uc);
+  sw_entries<L>(R, cur, sw_range(P, cur, h), gl, 0, uc);
   sw_fetch<X>(P, R, h, sb + stride + grp, o1, nxt);
   // the previous batch's record stores, issued at the top of the next
   // iteration ahead of its loads (vector-memory counters retire in order: a
@@ -456,23 +485,23 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
   for (; sb < o1; sb += stride) {  // wave-uniform
     *st_d = ds;
     *st_i = is;
-    if constexpr (!FIN) *st_d2 = ds2;
+    if constexpr (!FIN && L == 8) *st_d2 = ds2;
     const uint32_t bdc = sw_range(P, cur, h);
     double xv[kSweepPre];
     if (X) sw_xv(R, cur, uc, xv);
     uint32_t un[kSweepPre];
-    sw_entries(R, nxt, sw_range(P, nxt, h), gl, 0, un);
+    sw_entries<L>(R, nxt, sw_range(P, nxt, h), gl, 0, un);
     SwOcc nn;
     sw_fetch<X>(P, R, h, sb + 2 * stride + grp, o1, nn);
     SwAcc A;
-    sw_block<X, FIN>(colv, row0, cur, bdc, gl, 0, uc, xv, gj, A);
+    sw_block<X, FIN, L>(colv, row0, cur, bdc, gl, 0, uc, xv, gj, A);
     {
       const int e0 = (int)(bdc & 0xFFFFu), e1 = (int)(bdc >> 16);
-      for (int t0 = kSweepPre; e0 + kSweepLanes * t0 < e1; t0 += kSweepPre) {  // long chunk ranges
+      for (int t0 = kSweepPre; e0 + L * t0 < e1; t0 += kSweepPre) {  // long chunk ranges
         uint32_t ux[kSweepPre];
-        sw_entries(R, cur, bdc, gl, t0, ux);
+        sw_entries<L>(R, cur, bdc, gl, t0, ux);
         if (X) sw_xv(R, cur, ux, xv);
-        sw_block<X, FIN>(colv, row0, cur, bdc, gl, t0, ux, xv, gj, A);
+        sw_block<X, FIN, L>(colv, row0, cur, bdc, gl, t0, ux, xv, gj, A);
       }
     }
     // record fields: 0 plain, 1 ff, 2..7 the CorrVector sums sx, sy, sxx, syy,
@@ -487,7 +516,15 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
     // write P.sink
     const bool live = sb + grp < o1;
     double* rec = P.rec + ((int64_t)(cur.mt.x + (cur.mt.y & 0xFFFFu)) * P.n_chunks + h) * kSweepRec;
-    if constexpr (FIN) {
+    if constexpr (L == 16) {
+      // lane gl: double field gl (8 fields for finite data, 9 otherwise);
+      // lanes 0, 4, 8: integer fields 9..11
+      ds = sw_transpose16(dv, lane);
+      is = sw_transpose4_u64(iv, lane);
+      st_d = live && gl < (FIN ? 8 : 9) ? rec + gl : P.sink + lane;
+      st_i = live && (gl & 3) == 0 && gl < 12 ? reinterpret_cast<unsigned long long*>(rec) + 9 + (gl >> 2)
+                                               : reinterpret_cast<unsigned long long*>(P.sink) + 64 + lane;
+    } else if constexpr (FIN) {
       // lane (b2 b1 b0): double field 4 b2 + 2 b1 + b0; lanes with b0 = 0: integer field 9 + 2 b2 + b1
       ds = sw_transpose8_8(dv8, lane);
       is = sw_transpose4_u64_8(iv, lane);
@@ -515,7 +552,7 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
   }
   *st_d = ds;
   *st_i = is;
-  if constexpr (!FIN) *st_d2 = ds2;
+  if constexpr (!FIN && L == 8) *st_d2 = ds2;
 }
 
 // ---- 5. per item ---------------------------------------------------------------
@@ -648,15 +685,24 @@ hipError_t launch_sweep(const SweepParams& P0, hipStream_t st) {
                      P);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const dim3 grid((unsigned)P.n_nodes, (unsigned)P.n_chunks);
-  if (P.disc_cv && P.finite)
-    hipLaunchKernelGGL((sweep_column_kernel<true, true>), grid, dim3(kSweepWaves * 64), 16 * (size_t)P.chunk_rows, st,
-                       P);
-  else if (P.disc_cv)
-    hipLaunchKernelGGL((sweep_column_kernel<true, false>), grid, dim3(kSweepWaves * 64), 16 * (size_t)P.chunk_rows, st,
-                       P);
+  // lanes per occurrence by module size only (one numerical path per shape)
+#define NR_SWEEP_LAUNCH(L_)                                                                                    \
+  do {                                                                                                         \
+    if (P.disc_cv && P.finite)                                                                                 \
+      hipLaunchKernelGGL((sweep_column_kernel<true, true, L_>), grid, dim3(kSweepWaves * 64),                  \
+                         16 * (size_t)P.chunk_rows, st, P);                                                    \
+    else if (P.disc_cv)                                                                                        \
+      hipLaunchKernelGGL((sweep_column_kernel<true, false, L_>), grid, dim3(kSweepWaves * 64),                 \
+                         16 * (size_t)P.chunk_rows, st, P);                                                    \
+    else                                                                                                       \
+      hipLaunchKernelGGL((sweep_column_kernel<false, false, L_>), grid, dim3(kSweepWaves * 64),                \
+                         8 * (size_t)P.chunk_rows, st, P);                                                     \
+  } while (0)
+  if (P.k_max > kSweepWideK)
+    NR_SWEEP_LAUNCH(16);
   else
-    hipLaunchKernelGGL((sweep_column_kernel<false, false>), grid, dim3(kSweepWaves * 64), 8 * (size_t)P.chunk_rows,
-                       st, P);
+    NR_SWEEP_LAUNCH(8);
+#undef NR_SWEEP_LAUNCH
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sweep_finish_kernel, dim3((unsigned)((n_items + 3) / 4)), dim3(256),
                      4 * sizeof(double) * (size_t)P.k_max, st, P, n_items);

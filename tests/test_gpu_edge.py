@@ -49,3 +49,23 @@ def test_small_and_boundary_modules_vs_oracle(n_samples, sizes):
                        what=f"observed S={n_samples} {sizes}")
     assert_stats_close(_mask_two_node_noise(nulls, mi), _mask_two_node_noise(exp, mi),
                        what=f"nulls S={n_samples} {sizes}")
+
+
+@pytest.mark.parametrize("nonfinite", [False, True])
+def test_wide_modules_sixteen_lane_sweep_vs_oracle(nonfinite):
+    """Modules beyond kSweepWideK (1,024) nodes take the column sweep's
+    sixteen-lane path (sweep.hip, the C5 shape): finite data, and with a NaN
+    test correlation inside the wide module (the complete-case records)."""
+    lay, mi, disc, tx, tc, tn = _engine_case(n_nodes=2600, n_samples=20, sizes=(1100, 40), seed=5)
+    if nonfinite:
+        m0 = max(mi.mods_present, key=lambda m: mi.test_idx[m].size)
+        a, b = mi.test_idx[m0][3], mi.test_idx[m0][10]
+        tc = tc.copy()
+        tc[a, b] = tc[b, a] = np.nan
+    eng = _engine_from(mi, disc, tx, tc, tn)
+    seed = 31
+    nulls = eng.run(0, 4, seed)
+    pis = np.stack([prp.permute(np.arange(mi.null_idx.size), mi.null_idx.size, seed, p) for p in range(4)])
+    exp, obs = O.permutation_procedure(disc, tx, tc, tn, mi, pis.astype(np.int64))
+    assert_stats_close(eng.observed(), obs, what=f"observed, wide modules, nonfinite={nonfinite}")
+    assert_stats_close(nulls, exp, what=f"nulls, wide modules, nonfinite={nonfinite}")
