@@ -1,11 +1,15 @@
-"""The small class of summary-profile items (kernels.h kSmallDim): Lanczos
-dimension min(k, S) <= 112, two-wave workgroups, per-node arrays of modules
-longer than 112 nodes in the slot's scratch. Checked against the C++ LAPACK
-restatement on identical shuffles at the class's edges (k = 112 / 113, k = S,
-dual and primal items in one launch), through the non-finite path, and the
-packed 4-wave kernel's dual path, which the small class now takes over for
-S <= 112, at an S just above it; the large-module kernel (64 x 64
-super-tile Gram) on primal and dual modules, with non-finite columns."""
+"""The small-dimension summary-profile classes. The wave class (kernels.h
+kWaveDim, round 5) takes every launch whose Lanczos dimension min(k, S) is at
+most 111: one wave per item, the Gram in its MFMA accumulator registers,
+per-node arrays of modules longer than 112 nodes in the slot's scratch. The
+small class (kSmallDim: two-wave workgroups, packed Gram in scratch) keeps a
+dimension of exactly 112. Both are checked against the C++ LAPACK restatement
+on identical shuffles: the wave class at S = 60 (dual items with per-node
+arrays in scratch (200, 113) and in LDS (112, 61), k == S, primal items) and
+through the non-finite path; the small class with a 112-node primal module at
+S = 300. Also the packed 4-wave kernel's dual path at an S just above both
+classes, and the large-module kernel (64 x 64 super-tile Gram) on primal and
+dual modules, with non-finite columns."""
 import numpy as np
 import pytest
 
@@ -20,8 +24,8 @@ pytestmark = pytest.mark.gpu
 
 
 def test_small_class_edges_vs_cpp_oracle():
-    """S = 60: dual items with per-node arrays in scratch (200, 113 > 112),
-    in LDS (112, 61), k == S and primal items (59, 7)."""
+    """S = 60 (the wave class): dual items with per-node arrays in scratch
+    (200, 113 > 112), in LDS (112, 61), k == S and primal items (59, 7)."""
     lay, mi, disc, txs, tc, tn = _case([200, 113, 112, 61, 60, 59, 7], 60, 71, n_nodes=1500)
     eng = _engine_from(mi, disc, txs, tc, tn)
     nulls = eng.run(5, 29, 123)
@@ -32,8 +36,9 @@ def test_small_class_edges_vs_cpp_oracle():
 
 
 def test_small_class_primal_only_vs_cpp_oracle():
-    """S = 300 with every module of at most 112 nodes: primal items of the
-    small class only (Lanczos dimension k)."""
+    """S = 300 with every module of at most 112 nodes: the 112-node module
+    puts the launch on the small class (Lanczos dimension 112 > kWaveDim),
+    primal items only."""
     lay, mi, disc, txs, tc, tn = _case([112, 96, 64, 33, 16], 300, 73, n_nodes=1200)
     eng = _engine_from(mi, disc, txs, tc, tn)
     nulls = eng.run(0, 16, 5)
@@ -47,7 +52,7 @@ def test_small_class_primal_only_vs_cpp_oracle():
 
 def test_small_class_nonfinite_column_gives_na():
     """A NaN data column of a module's node: that module's summary-profile
-    statistics are NA (src/netStats.cpp:229-235) on the small class too."""
+    statistics are NA (src/netStats.cpp:229-235) on the wave class too."""
     lay, mi, disc, txs, tc, tn = _case([150, 40, 20], 50, 75, n_nodes=600)
     txs = txs.copy()
     m0 = mi.mods_present[0]
