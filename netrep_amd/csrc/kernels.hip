@@ -1608,7 +1608,12 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   // geometric decay since the previous check predicts convergence (at most 8
   // steps on). Offline study on C3 null items (tools/sim_lanczos.py): 36.0
   // steps/item vs 37.9 for a fixed 8-step cadence, same number of checks.
-  int next_check = mcap < 16 ? mcap : 16;
+  // (the wave class checks first at step 20: its lone wave pays for every
+  // check's Sturm passes in full; C2 shape 1.908 -> 1.841 ms per 256
+  // permutations, 0.02% more steps. The 4-wave kernels keep 16: at C3, 20
+  // and 24 measured -0.2% and +0.9%, profiles/r05/firstcheck/)
+  constexpr int first_check = NW == 1 ? 20 : 16;
+  int next_check = mcap < first_check ? mcap : first_check;
   int prev_j = 0;  // lane 0 of wave 0 only
   double prev_r = 0.0;
   double hint_theta = 0.0, hint_r = 0.0;  // previous check, every lane of wave 0 (warm start)
