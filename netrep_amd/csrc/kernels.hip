@@ -2141,6 +2141,7 @@ __device__ __forceinline__ void gram_wave_epilogue(const nr_f64x4 (&T)[kWaveTile
 // row groups (two permlane swaps) into yup; out = ylo + yup. A fixed order
 // throughout: bitwise reproducible. Returns sum_r y_r out_r if y (every lane).
 // SQ: out_r = sum_c G_rc^2 over c < n instead (start column norms; x unused).
+constexpr int kRowGroup = 3;  // tile rows per branch of wave_matvec
 template <bool SQ>
 __device__ __forceinline__ double wave_matvec(const nr_f64x4 (&T)[kWaveTiles], int nb, int n, const double* x,
                                               double* out, const double* y, double* ylo, double* yup) {
@@ -2151,29 +2152,38 @@ __device__ __forceinline__ double wave_matvec(const nr_f64x4 (&T)[kWaveTiles], i
   for (int I = 0; I < kWaveBlocks; ++I) {
     au[I] = 0.0;
     xc[I] = 0.0;
-    if (I < nb) xc[I] = SQ ? (16 * I + i16 < n ? 1.0 : 0.0) : x[16 * I + i16];
+    if (I < nb + kRowGroup - 1) xc[I] = SQ ? (16 * I + i16 < n ? 1.0 : 0.0) : x[16 * I + i16];
   }
   const int rg = 4 * (((lane >> 3) & 1) * 2 + ((lane >> 2) & 1));  // row offset of rg_row_reduce's group
   // one pass over the tiles, each value read once: tile row I's lower sums
   // (reduced and stored when the row is done) and, below the diagonal, the
   // mirrored sums of the tile columns J < I
+  // tile rows in groups of three, one branch on nb per group: the rows'
+  // reductions interleave (their DPP wait states filled by each other). A row
+  // of a group past nb has zero tiles and x, and writes ylo rows >= n only.
+  // (C2 shape per 256 permutations: one row per branch 1.860 ms, groups of 2
+  // 1.822, 3 1.797, 4 1.842; no branch at all spilled inside the Lanczos
+  // loop. profiles/r05/rowg/)
 #pragma unroll
-  for (int I = 0; I < kWaveBlocks; ++I) {
-    if (I >= nb) break;
-    double xri[4], a[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int I0 = 0; I0 < kWaveBlocks; I0 += kRowGroup) {
+    if (I0 >= nb) break;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) xri[r] = SQ ? (16 * I + kk + 4 * r < n ? 1.0 : 0.0) : x[16 * I + kk + 4 * r];
+    for (int I = I0; I < I0 + kRowGroup && I < kWaveBlocks; ++I) {
+      double xri[4], a[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int J = 0; J <= I; ++J)
+      for (int r = 0; r < 4; ++r) xri[r] = SQ ? (16 * I + kk + 4 * r < n ? 1.0 : 0.0) : x[16 * I + kk + 4 * r];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double g = tile_val(T[wave_tile(I, J)], r);
-        const double gg = SQ ? g * g : g;
-        a[r] = fma(gg, xc[J], a[r]);
-        if (J < I) au[J] = fma(gg, xri[r], au[J]);
-      }
-    const double v = rg_row_reduce(a, lane);
-    if ((lane & 3) == 0) ylo[16 * I + kk + rg] = v;
+      for (int J = 0; J <= I; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double g = tile_val(T[wave_tile(I, J)], r);
+          const double gg = SQ ? g * g : g;
+          a[r] = fma(gg, xc[J], a[r]);
+          if (J < I) au[J] = fma(gg, xri[r], au[J]);
+        }
+      const double v = rg_row_reduce(a, lane);
+      if ((lane & 3) == 0) ylo[16 * I + kk + rg] = v;
+    }
   }
 #pragma unroll
   for (int J = 0; J < kWaveBlocks; ++J) {
