@@ -2185,9 +2185,10 @@ __device__ __forceinline__ double wave_matvec(const nr_f64x4 (&T)[kWaveTiles], i
       if ((lane & 3) == 0) ylo[16 * I + kk + rg] = v;
     }
   }
+  // (no branch: a column past nb sums zeros into yup rows >= n; the seven
+  // swap chains interleave)
 #pragma unroll
   for (int J = 0; J < kWaveBlocks; ++J) {
-    if (J >= nb) break;
     double a = nr_swap16_sum(au[J], au[J]);
     a = nr_swap32_sum(a, a);
     if (kk == 0) yup[16 * J + i16] = a;
