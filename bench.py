@@ -282,6 +282,19 @@ def table_bytes(sizes):
 # column reading its rows there -- so no random-gather ceiling applies; the
 # roofline is SURVEY.md 8d's network bytes against HBM peak.
 NET_KERNEL = "network_sweep"
+# rocprofv3 names of what the engine's two timers measure (timer 0: the
+# network launches, timer 1: the summary-profile launches), by path
+NET_SYMBOLS = "nr::sweep_column_kernel + sweep_cols/scan/prep/finish_kernel (the column sweep, one batch)"
+
+
+def profile_symbol(table, sizes, n_samples):
+    """The summary-profile kernel a launch of these shapes runs (engine.hip
+    plan_profile / table_wanted: one numerical path per shape)."""
+    if table:
+        return "nr::module_profile_table_kernel"
+    if min(max(sizes), n_samples) <= 111:
+        return "nr::module_profile_wave_kernel"
+    return "nr::module_profile_big_kernel + nr::module_profile_packed4_kernel (the summary-profile launches)"
 NET_UNITS = ("achieved = SURVEY.md 8d network bytes 4k + 8k(k-1)/2 + 8k^2 per module-permutation x the "
              "launch's items / HIP-event time of the sweep's five kernels (sweep.hip)")
 
@@ -515,7 +528,8 @@ def run_c5(args, world, rank, local):
     b_launch = int(round(P / max(l1, 1)))
     if mk["achieved"] is not None:
         avg1 = ms1 / max(l1, 1)
-        line["roofline"] = {"kernel": "module_profile_kernel", "bound": "mfma", "achieved": round(mk["achieved"], 4),
+        line["roofline"] = {"kernel": profile_symbol(False, sizes, s), "timer": "module_profile_kernel",
+                            "bound": "mfma", "achieved": round(mk["achieved"], 4),
                             "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(mk["frac"], 6),
                             "avg_ms": avg1, "algorithmic_bytes": round(prof_b * b_launch),
                             "launch_permutations": b_launch,
@@ -589,8 +603,10 @@ def main():
     # -- secondary record: network-only (C4) on the same matrices ---------------
     secondary = None
     if eng2 is not None:
-        B2 = 1024
-        P2 = 16 * B2
+        # C4's own launch size (5,120 permutations: the committed PMC pass of
+        # the sweep, profiles/pmc_traffic.json, is of this launch)
+        B2 = 5120
+        P2 = 4 * B2
         eng2.set_batch(B2)
         el2, ch2, tot2 = time_steps(eng2, world, rank, args.secondary_steps, 1, P2, args.seed + 1,
                                     2 * 10**12 + rank * P2)
@@ -606,7 +622,7 @@ def main():
                 "value": tot2 / el2, "unit": "permutations/sec", "steps": args.secondary_steps,
                 "perms_per_step": P2, "launch_batch": B2, "ms_per_step": el2 / args.secondary_steps * 1e3,
                 "finite_fraction": fin2,
-                "roofline": {"kernel": NET_KERNEL, "bound": "hbm", "avg_ms": ms2 / max(l2, 1),
+                "roofline": {"kernel": NET_SYMBOLS, "timer": NET_KERNEL, "bound": "hbm", "avg_ms": ms2 / max(l2, 1),
                              "achieved": net_b * B2 / t2 / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": net_b * B2 / t2 / 1e9 / HBM_PEAK_GBS,
                              "algorithmic_bytes": round(net_b * B2), "units_note": NET_UNITS},
@@ -670,7 +686,9 @@ def main():
             kv["frac"] = kv["achieved"] / kv["peak"]
         dom_name = max(kernels, key=lambda n: kernels[n]["avg_ms"])
         dom = kernels[dom_name]
-        roofline = {"kernel": dom_name, "bound": dom["bound"], "achieved": round(dom["achieved"], 4),
+        symbol = (NET_SYMBOLS if dom_name == NET_KERNEL
+                  else profile_symbol(bool(table), lay.module_sizes, meta["n_samples"]))
+        roofline = {"kernel": symbol, "timer": dom_name, "bound": dom["bound"], "achieved": round(dom["achieved"], 4),
                     "peak": dom["peak"], "unit": dom["unit"], "frac": round(dom["frac"], 6),
                     "avg_ms": dom["avg_ms"], "algorithmic_bytes": dom["algorithmic_bytes"],
                     "units_note": dom.get("units_note")}

@@ -97,8 +97,13 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src);
  * a scatter + all-gather of peer copies over the full xGMI mesh (each
  * destination receives one piece from the source and the other n - 2 pieces
  * from the destinations that received them; every link carries 1/(n-1) of
- * the bytes per phase). Contexts must be distinct; several may share a GPU. */
+ * the bytes per phase). Contexts must be distinct; several may share a GPU.
+ * Peer access is enabled per GPU pair; a pair without it is copied through
+ * host memory by the runtime (slower, still correct) and counted by
+ * nr_peer_staged_pairs. The calling thread's current device is restored. */
 int nr_broadcast_dataset(nr_ctx* const* ctxs, int n);
+/* Ordered GPU pairs found without peer access so far in this process. */
+int nr_peer_staged_pairs(int* n);
 
 /* 1 if corr and net of the resident dataset are exactly symmetric. */
 int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric);
@@ -255,6 +260,23 @@ int nr_synchronize(nr_ctx* ctx);
  * is a measurement run, not a timed one. */
 int nr_set_stamps(nr_ctx* ctx, int enable);
 int nr_get_stamps(nr_ctx* ctx, uint64_t* cycles);
+
+/* Per-batch work buffers (column-sweep sets, profile-slot scratch, device
+ * output and shuffle-table buffers): nr_release_scratch frees them (the next
+ * run reallocates), nr_scratch_bytes reports what a context holds. The
+ * reference-interface layer releases them whenever it pools a context. */
+int nr_release_scratch(nr_ctx* ctx);
+int nr_scratch_bytes(const nr_ctx* ctx, int64_t* bytes);
+/* A context's own host-thread count (nr_ctx_set_host_threads). */
+int nr_ctx_get_host_threads(const nr_ctx* ctx, int* n);
+
+/* Test knobs, process-wide; neither changes a result. NR_DEBUG_SWEEP_MAX_OCC:
+ * the column sweep's sub-batch bound in occurrences (value <= 0 restores the
+ * default, 64M). NR_DEBUG_FAIL_SWEEP_ALLOC: the value-th column-sweep buffer
+ * allocation from now fails with NR_ERR_OOM (0: off). */
+#define NR_DEBUG_SWEEP_MAX_OCC 1
+#define NR_DEBUG_FAIL_SWEEP_ALLOC 2
+int nr_debug_set(int what, int64_t value);
 
 /* ---- reference-interface layer ----------------------------------------- */
 /* Names are arrays of NUL-terminated strings. moduleAssignments is the named
@@ -413,14 +435,23 @@ int netrep_CheckFinite(const double* mat, int64_t nrow, int64_t ncol);
  * netrep_IntermediateProperties and the dataset of netrep_NetProps stay
  * resident in HBM while later calls name the same host arrays (same
  * pointers and shape, and the same fingerprint of every element, hashed on
- * the call's host threads); contexts (streams, slot scratch) are pooled
- * across calls, and a pooled context is reset to the defaults (no dataset,
- * no cancel request, the process-wide host-thread count). A changed array
+ * the process-wide host threads of nr_set_host_threads -- a full pass over
+ * the host arrays at memory bandwidth, the price of reuse; a sampled check
+ * of 4,096 elements per array runs first, so a changed array skips the full
+ * pass); contexts (streams) are pooled across calls, and a pooled context is
+ * reset to the defaults (no dataset, no per-batch work buffers, no cancel
+ * request, the process-wide host-thread count). A changed array
  * is uploaded again. netrep_ReleaseResident frees all of it (the R glue calls
  * it when modulePreservation / networkProperties return); a
  * netrep_PermutationProcedure call that runs out of device memory releases
  * the resident datasets and retries once before returning NR_ERR_OOM. */
 void netrep_ReleaseResident(void);
+/* The pooled contexts (idle between calls): how many, the device bytes of
+ * per-batch work buffers they hold (0: released), and the range of their
+ * host-thread counts (each equals nr_get_host_threads after a call). With
+ * no pooled context the thread range is 0, 0. */
+int netrep_PoolInfo(int64_t* n_pooled, int64_t* scratch_bytes, int32_t* host_threads_min,
+                    int32_t* host_threads_max);
 
 /* Last error of the reference-interface layer (thread-local). */
 const char* netrep_last_error(void);

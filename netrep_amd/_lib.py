@@ -123,7 +123,15 @@ SIGNATURES = {
                                                 _i32, _u64, _u32p, _i64, _dp, _dp]),
     "netrep_ReadRDSMatrix": (_int, [C.c_char_p, C.c_char_p, _i64p, _i64p, _dp, C.c_char_p, _i64, _i64p]),
     "netrep_DiscardPrefetch": (None, []),
+    "nr_release_scratch": (_int, [_p]),
+    "nr_scratch_bytes": (_int, [_p, _i64p]),
+    "nr_ctx_get_host_threads": (_int, [_p, _intp]),
+    "nr_debug_set": (_int, [_int, _i64]),
+    "nr_peer_staged_pairs": (_int, [_intp]),
+    "netrep_PoolInfo": (_int, [_i64p, _i64p, _i32p, _i32p]),
 }
+NR_DEBUG_SWEEP_MAX_OCC = 1
+NR_DEBUG_FAIL_SWEEP_ALLOC = 2
 
 _lib = None
 

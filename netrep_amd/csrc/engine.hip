@@ -110,6 +110,8 @@ struct nr_ctx {
   size_t out2_cap = 0;
   double* h_stage2 = nullptr;
   size_t stage2_cap = 0;
+  double* h_scale = nullptr;  // nr_scale's pinned staging (4 column chunks)
+  size_t scale_cap = 0;
   hipEvent_t ev_copy[2] = {nullptr, nullptr};
 
   // The observed statistics' own lane (nr_observed_async): stream, scratch and
@@ -627,6 +629,10 @@ int launch_nets(nr_ctx* ctx, nr::NetParams np, const int32_t* d_order, const std
 // occurrence ids, bounded buffers); an item's statistics do not depend on
 // the batch it runs in, so neither do the results.
 constexpr int64_t kSweepMaxOcc = (int64_t)64 << 20;
+// nr_debug_set test knobs (neither changes a result): a smaller sub-batch
+// bound, and an injected failure of the n-th sweep buffer allocation.
+std::atomic<int64_t> g_sweep_max_occ{kSweepMaxOcc};
+std::atomic<int> g_fail_sweep_alloc{0};
 constexpr int64_t kSweepMaxRecBytes = (int64_t)32 << 30;  // the (occurrence, chunk) records of one sub-batch
 
 int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const Lane& ln);
@@ -637,7 +643,7 @@ int launch_sweep_batch(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, con
   const int64_t chunks =
       (ctx->n_nodes + nr::sweep_chunk_rows(ctx->n_nodes, np.disc_cv ? 16 : 8) - 1) /
       nr::sweep_chunk_rows(ctx->n_nodes, np.disc_cv ? 16 : 8);
-  const int64_t max_occ = std::min<int64_t>(kSweepMaxOcc, kSweepMaxRecBytes / (chunks * 8 * nr::kSweepRec));
+  const int64_t max_occ = std::min<int64_t>(g_sweep_max_occ.load(), kSweepMaxRecBytes / (chunks * 8 * nr::kSweepRec));
   const int64_t per = std::max<int64_t>(1, max_occ / std::max<int64_t>(ctx->n_node_total, 1));
   for (int64_t p0 = 0; p0 < n_perm; p0 += per) {
     const int64_t np_sub = std::min(per, n_perm - p0);
@@ -656,20 +662,25 @@ int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const
   nr::SweepParams P{};
   P.chunk_rows = nr::sweep_chunk_rows(ctx->n_nodes, np.disc_cv ? 16 : 8);
   P.n_chunks = (int32_t)((ctx->n_nodes + P.chunk_rows - 1) / P.chunk_rows);
-  auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t per) -> int {
-    (void)cap;
+  // Every buffer of a set is freed before it is reallocated, so a set's
+  // capacity is committed only once the whole chain has succeeded: after an
+  // allocation failure the capacity reads 0 and the next call reallocates
+  // instead of launching on the freed (null) pointers.
+  auto grow = [&](auto*& ptr, size_t need, size_t per) -> int {
     dfree(ptr);
+    if (g_fail_sweep_alloc.load() > 0 && g_fail_sweep_alloc.fetch_sub(1) == 1)
+      return fail(ctx, NR_ERR_OOM, "sweep buffers: injected allocation failure (nr_debug_set)");
     NR_HIP(ctx, hipMalloc((void**)&ptr, std::max<size_t>(need, 1) * per));
     return NR_OK;
   };
   int rc;
   if (n_occ > b.occ_cap || P.n_chunks > b.chunk_cap) {
-    size_t c = 0;
-    if ((rc = grow(b.col, c, n_occ, 4)) || (rc = grow(b.rank, c, n_occ, 4)) ||
-        (rc = grow(b.sorted, c, n_occ, 4)) || (rc = grow(b.lrank, c, n_occ, 4)) ||
-        (rc = grow(b.meta, c, n_occ, 2 * sizeof(uint4))) ||
-        (rc = grow(b.bndh, c, P.n_chunks > 2 ? n_occ : 0, 4 * (size_t)P.n_chunks)) ||
-        (rc = grow(b.rec, c, n_occ, 8 * nr::kSweepRec * (size_t)P.n_chunks)))
+    b.occ_cap = 0;
+    b.chunk_cap = 0;
+    if ((rc = grow(b.col, n_occ, 4)) || (rc = grow(b.rank, n_occ, 4)) || (rc = grow(b.sorted, n_occ, 4)) ||
+        (rc = grow(b.lrank, n_occ, 4)) || (rc = grow(b.meta, n_occ, 2 * sizeof(uint4))) ||
+        (rc = grow(b.bndh, P.n_chunks > 2 ? n_occ : 0, 4 * (size_t)P.n_chunks)) ||
+        (rc = grow(b.rec, n_occ, 8 * nr::kSweepRec * (size_t)P.n_chunks)))
       return rc;
     b.occ_cap = n_occ;
     b.chunk_cap = P.n_chunks;
@@ -680,8 +691,8 @@ int launch_sweep_sub(nr_ctx* ctx, const nr::NetParams& np, int64_t n_perm, const
   }
   const size_t n_cols = (size_t)ctx->n_nodes + 1;
   if (n_cols > b.col_cap) {
-    size_t c = 0;
-    if ((rc = grow(b.count, c, n_cols, 4)) || (rc = grow(b.col_off, c, n_cols, 4)) || (rc = grow(b.dabs, c, n_cols, 8)))
+    b.col_cap = 0;
+    if ((rc = grow(b.count, n_cols, 4)) || (rc = grow(b.col_off, n_cols, 4)) || (rc = grow(b.dabs, n_cols, 8)))
       return rc;
     b.col_cap = n_cols;
   }
@@ -1184,6 +1195,7 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   dfree(ctx->d_obs);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_stage2) (void)hipHostFree(ctx->h_stage2);
+  if (ctx->h_scale) (void)hipHostFree(ctx->h_scale);
   for (auto& ev : ctx->ev)
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : ctx->ev_copy)
@@ -1220,8 +1232,8 @@ int nr_h2d_bytes(int64_t* bytes) {
 }
 
 // Copy n doubles with up to `threads` host threads (pageable -> pinned staging).
-static void parallel_copy(double* dst, const double* src, int64_t n, int threads) {
-  const int64_t min_part = (int64_t)1 << 20;  // 8 MiB per thread at least
+static void parallel_copy(double* dst, const double* src, int64_t n, int threads,
+                          int64_t min_part = (int64_t)1 << 20 /* 8 MiB per thread at least */) {
   const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n / min_part));
   if (nt == 1) {
     std::memcpy(dst, src, (size_t)n * sizeof(double));
@@ -1570,22 +1582,24 @@ int nr_copy_dataset(nr_ctx* dst, const nr_ctx* src) {
 // all-gather reads every destination from every other): direct copies over
 // the xGMI links instead of copies staged through host memory
 // (src/permutations.cpp:335-380 is the reference's one-process parallel
-// section this replaces). Enabled once per ordered pair per process; a pair
-// without peer access is an error, not a silent host-staged copy.
+// section this replaces). Enabled once per ordered pair per process. A pair
+// without peer access still works -- hipMemcpyPeerAsync stages it through
+// host memory -- at PCIe speed; such pairs are recorded
+// (nr_peer_staged_pairs) instead of failing the broadcast.
 static std::mutex g_peer_mu;
-static std::set<std::pair<int, int>> g_peer_on;
+static std::set<std::pair<int, int>> g_peer_on, g_peer_staged;
 
 static int enable_peer_access(nr_ctx* err_ctx, const std::vector<int>& devs) {
   std::lock_guard<std::mutex> lk(g_peer_mu);
   for (int a : devs)
     for (int b : devs) {
-      if (a == b || g_peer_on.count({a, b})) continue;
+      if (a == b || g_peer_on.count({a, b}) || g_peer_staged.count({a, b})) continue;
       int can = 0;
       NR_HIP(err_ctx, hipDeviceCanAccessPeer(&can, a, b));
-      if (!can)
-        return fail(err_ctx, NR_ERR_HIP,
-                    "GPU " + std::to_string(a) + " cannot access GPU " + std::to_string(b) +
-                        " as a peer (no xGMI path): the dataset broadcast needs peer access");
+      if (!can) {
+        g_peer_staged.insert({a, b});
+        continue;
+      }
       NR_HIP(err_ctx, hipSetDevice(a));
       const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
       if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return hip_fail(err_ctx, e, "hipDeviceEnablePeerAccess");
@@ -1595,8 +1609,27 @@ static int enable_peer_access(nr_ctx* err_ctx, const std::vector<int>& devs) {
   return NR_OK;
 }
 
+int nr_peer_staged_pairs(int* n) {
+  if (!n) return NR_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(g_peer_mu);
+  *n = (int)g_peer_staged.size();
+  return NR_OK;
+}
+
+// The calling thread's current device, restored on every return path.
+struct DeviceRestore {
+  int dev = -1;
+  DeviceRestore() {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~DeviceRestore() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+};
+
 int nr_broadcast_dataset(nr_ctx* const* ctxs, int n) {
   if (!ctxs || n < 1) return NR_ERR_INVALID;
+  DeviceRestore restore;
   nr_ctx* src = ctxs[0];
   if (!src) return NR_ERR_INVALID;
   for (int g = 1; g < n; ++g)
@@ -1709,7 +1742,6 @@ int nr_broadcast_dataset(nr_ctx* const* ctxs, int n) {
     d->net_finite = src->net_finite;
     d->table_ms = src->table_ms;
   }
-  (void)hipSetDevice(src->device);
   return NR_OK;
 }
 
@@ -1720,6 +1752,91 @@ int nr_clear_dataset(nr_ctx* ctx) {
   reset_dataset(ctx);
   ctx->cancel = false;  // a context cancelled after its run returned starts clean
   return NR_OK;
+}
+
+// The per-batch work buffers (the column sweep's sets, the profile slots'
+// scratch, the device output and shuffle-table buffers); the next run
+// reallocates what it needs. The reference-interface layer calls this when
+// it pools a context, so no HBM is held between its calls (a
+// sub-batch's sweep records alone may take tens of GB).
+int nr_release_scratch(nr_ctx* ctx) {
+  if (!ctx) return NR_ERR_INVALID;
+  NR_HIP(ctx, hipSetDevice(ctx->device));
+  NR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  sync_obs(ctx);
+  for (auto& b : ctx->sweep) {
+    dfree(b.col);
+    dfree(b.rank);
+    dfree(b.count);
+    dfree(b.col_off);
+    dfree(b.sorted);
+    dfree(b.meta);
+    dfree(b.bndh);
+    dfree(b.lrank);
+    dfree(b.dabs);
+    dfree(b.zs);
+    dfree(b.rec);
+    b.occ_cap = b.col_cap = 0;
+    b.chunk_cap = 0;
+  }
+  dfree(ctx->d_out);
+  ctx->out_cap = 0;
+  dfree(ctx->d_out2);
+  ctx->out2_cap = 0;
+  dfree(ctx->d_pi);
+  ctx->pi_cap = 0;
+  dfree(ctx->d_scratch);
+  ctx->scratch_cap = 0;
+  dfree(ctx->d_net_scratch);
+  ctx->net_scratch_cap = 0;
+  dfree(ctx->obs_scratch);
+  ctx->obs_scratch_cap = 0;
+  dfree(ctx->obs_net_scratch);
+  ctx->obs_net_cap = 0;
+  dfree(ctx->d_obs);
+  ctx->obs_cap = 0;
+  return NR_OK;
+}
+
+int nr_scratch_bytes(const nr_ctx* ctx, int64_t* bytes) {
+  if (!ctx || !bytes) return NR_ERR_INVALID;
+  int64_t t = 0;
+  for (const auto& b : ctx->sweep) {
+    if (b.col) t += (int64_t)b.occ_cap * (4 * 4 + 2 * (int64_t)sizeof(uint4));
+    if (b.bndh) t += (int64_t)b.occ_cap * 4 * b.chunk_cap;
+    if (b.rec) t += (int64_t)b.occ_cap * 8 * nr::kSweepRec * b.chunk_cap;
+    if (b.count) t += (int64_t)b.col_cap * 16;
+    if (b.zs) t += (4 + 256) * 8;
+  }
+  if (ctx->d_out) t += (int64_t)ctx->out_cap * 8;
+  if (ctx->d_out2) t += (int64_t)ctx->out2_cap * 8;
+  if (ctx->d_pi) t += (int64_t)ctx->pi_cap * 4;
+  if (ctx->d_scratch) t += (int64_t)ctx->scratch_cap * 8;
+  if (ctx->d_net_scratch) t += (int64_t)ctx->net_scratch_cap * 8;
+  if (ctx->obs_scratch) t += (int64_t)ctx->obs_scratch_cap * 8;
+  if (ctx->obs_net_scratch) t += (int64_t)ctx->obs_net_cap * 8;
+  if (ctx->d_obs) t += (int64_t)ctx->obs_cap * 8;
+  *bytes = t;
+  return NR_OK;
+}
+
+int nr_ctx_get_host_threads(const nr_ctx* ctx, int* n) {
+  if (!ctx || !n) return NR_ERR_INVALID;
+  *n = ctx->host_threads;
+  return NR_OK;
+}
+
+int nr_debug_set(int what, int64_t value) {
+  switch (what) {
+    case NR_DEBUG_SWEEP_MAX_OCC:
+      g_sweep_max_occ = value > 0 ? value : kSweepMaxOcc;
+      return NR_OK;
+    case NR_DEBUG_FAIL_SWEEP_ALLOC:
+      g_fail_sweep_alloc = (int)std::max<int64_t>(0, value);
+      return NR_OK;
+    default:
+      return NR_ERR_INVALID;
+  }
 }
 
 int nr_dataset_symmetric(nr_ctx* ctx, int* symmetric) {
@@ -2032,19 +2149,54 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
   return rc;
 }
 
+// Scale (src/scale.cpp:38-45) of a host matrix: column chunks of ~8 MiB
+// through the context's pinned staging buffers, double-buffered. Host threads
+// copy chunk i into pinned memory while the copy engine and the kernel work
+// on chunk i-1, then copy chunk i-1's result out of pinned memory. The
+// caller's pageable arrays are never handed to the DMA engine directly (that
+// ran at ~5 GB/s: 31 ms for 20k x 500, profiles/r05/props/).
 int nr_scale(nr_ctx* ctx, const double* data, int64_t n_samples, int64_t n_nodes, double* scaled) {
   if (!ctx || !data || !scaled || n_samples <= 0 || n_nodes <= 0) return NR_ERR_INVALID;
   NR_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t bytes = (size_t)(n_samples * n_nodes) * sizeof(double);
-  double *din = nullptr, *dout = nullptr;
-  NR_HIP(ctx, hipMalloc((void**)&din, bytes));
-  hipError_t e = hipMalloc((void**)&dout, bytes);
-  if (e == hipSuccess) e = h2d_async(din, data, bytes, ctx->stream);
-  if (e == hipSuccess) e = nr::launch_scale(din, dout, n_samples, n_nodes, ctx->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(scaled, dout, bytes, hipMemcpyDeviceToHost, ctx->stream);
+  const int64_t S = n_samples;
+  const int64_t cols = std::max<int64_t>(1, std::min<int64_t>(n_nodes, ((int64_t)1 << 20) / S));
+  const int64_t chunk = cols * S;  // doubles per chunk
+  if (int rc = ensure_stage(ctx, ctx->h_scale, ctx->scale_cap, (size_t)(4 * chunk))) return rc;
+  double* hin[2] = {ctx->h_scale, ctx->h_scale + chunk};
+  double* hout[2] = {ctx->h_scale + 2 * chunk, ctx->h_scale + 3 * chunk};
+  double* dbuf = nullptr;
+  NR_HIP(ctx, hipMalloc((void**)&dbuf, (size_t)(4 * chunk) * sizeof(double)));
+  double* din[2] = {dbuf, dbuf + chunk};
+  double* dout[2] = {dbuf + 2 * chunk, dbuf + 3 * chunk};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  for (int b = 0; b < 2 && e == hipSuccess; ++b) e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
+  const int threads = ctx->host_threads;
+  const int64_t n_chunks = (n_nodes + cols - 1) / cols;
+  auto drain = [&](int64_t i) {  // chunk i's result from pinned memory to the caller
+    const int b = (int)(i & 1);
+    const int64_t c0 = i * cols, nc = std::min(cols, n_nodes - c0);
+    e = hipEventSynchronize(ev[b]);
+    if (e == hipSuccess) parallel_copy(scaled + c0 * S, hout[b], nc * S, threads, (int64_t)1 << 17);
+  };
+  for (int64_t i = 0; i < n_chunks && e == hipSuccess; ++i) {
+    const int b = (int)(i & 1);
+    const int64_t c0 = i * cols, nc = std::min(cols, n_nodes - c0);
+    // hin[b] / hout[b] were last used by chunk i-2, drained (event waited) in iteration i-1
+    parallel_copy(hin[b], data + c0 * S, nc * S, threads, (int64_t)1 << 17);
+    e = h2d_async(din[b], hin[b], (size_t)(nc * S) * sizeof(double), ctx->stream);
+    if (e == hipSuccess) e = nr::launch_scale(din[b], dout[b], S, nc, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(hout[b], dout[b], (size_t)(nc * S) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(ev[b], ctx->stream);
+    if (e == hipSuccess && i >= 1) drain(i - 1);
+  }
+  if (e == hipSuccess) drain(n_chunks - 1);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  (void)hipFree(din);
-  if (dout) (void)hipFree(dout);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (hipEvent_t x : ev)
+    if (x) (void)hipEventDestroy(x);
+  (void)hipFree(dbuf);
   if (e != hipSuccess) return hip_fail(ctx, e, "scale");
   return NR_OK;
 }

@@ -118,7 +118,8 @@ int open_ctx(int device, CtxPtr& out) {
   return NR_OK;
 }
 
-// Back to the pool without its dataset (HBM is not held between calls).
+// Back to the pool without its dataset or its per-batch work buffers (HBM is
+// not held between calls).
 void give_ctx(CtxPtr& c) {
   if (!c) return;
   std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -128,7 +129,7 @@ void give_ctx(CtxPtr& c) {
   // run had already returned); the host-thread count goes back to the
   // process default, so the next call's staging does not inherit nCores
   if (it == g_ctx_device.end() || g_pool.size() >= kPoolMax || nr_clear_dataset(c.get()) != NR_OK ||
-      nr_ctx_set_host_threads(c.get(), nr_get_host_threads()) != NR_OK) {
+      nr_release_scratch(c.get()) != NR_OK || nr_ctx_set_host_threads(c.get(), nr_get_host_threads()) != NR_OK) {
     if (it != g_ctx_device.end()) g_ctx_device.erase(it);
     c.reset();
     return;
@@ -182,17 +183,36 @@ uint64_t fingerprint(const double* a, int64_t n) {
   return h;
 }
 
+// A cheap first look: 4,096 evenly spaced elements of the array (first and
+// last included). A changed array usually fails here, and then the full hash
+// is not computed at all; a match still needs the full hash.
+uint64_t sampled_fingerprint(const double* a, int64_t n) {
+  uint64_t h = 0x13198A2E03707344ull ^ (uint64_t)n;
+  if (!a || n <= 0) return h;
+  const int64_t m = std::min<int64_t>(n, 4096);
+  for (int64_t t = 0; t < m; ++t) {
+    const int64_t i = m == 1 ? 0 : (int64_t)((__int128)t * (n - 1) / (m - 1));
+    h += fp_chunk(a + i, 0, 1) * (uint64_t)(2 * t + 1);
+  }
+  return h;
+}
+
 struct Resident {
   CtxPtr ctx;
   const double *data = nullptr, *corr = nullptr, *net = nullptr;
   int64_t n_samples = 0, n_nodes = 0;
-  uint64_t fp = 0;
+  uint64_t fp = 0, sfp = 0;
   static uint64_t fp_of(const double* data, const double* corr, const double* net, int64_t s, int64_t n) {
     return fingerprint(corr, n * n) * 3 + fingerprint(net, n * n) * 5 + fingerprint(data, s * n) * 7;
   }
+  static uint64_t sfp_of(const double* data, const double* corr, const double* net, int64_t s, int64_t n) {
+    return sampled_fingerprint(corr, n * n) * 3 + sampled_fingerprint(net, n * n) * 5 +
+           sampled_fingerprint(data, s * n) * 7;
+  }
   bool holds(const double* d, const double* c, const double* nt, int64_t s, int64_t n) const {
-    return ctx && data == d && corr == c && net == nt && n_nodes == n && (d == nullptr || n_samples == s) &&
-           fp == fp_of(d, c, nt, d ? s : 0, n);
+    if (!(ctx && data == d && corr == c && net == nt && n_nodes == n && (d == nullptr || n_samples == s))) return false;
+    const int64_t ss = d ? s : 0;
+    return sfp == sfp_of(d, c, nt, ss, n) && fp == fp_of(d, c, nt, ss, n);
   }
   void keep(CtxPtr c, const double* d, const double* cr, const double* nt, int64_t s, int64_t n) {
     ctx = std::move(c);
@@ -202,6 +222,7 @@ struct Resident {
     n_samples = d ? s : 0;
     n_nodes = n;
     fp = fp_of(d, cr, nt, n_samples, n);
+    sfp = sfp_of(d, cr, nt, n_samples, n);
   }
   void drop() {
     give_ctx(ctx);
@@ -376,6 +397,27 @@ void netrep_ReleaseResident(void) {
     for (Pooled& p : all) g_ctx_device.erase(p.ctx.get());
   }
   all.clear();  // contexts destroyed while the runtime is alive
+}
+
+int netrep_PoolInfo(int64_t* n_pooled, int64_t* scratch_bytes, int32_t* host_threads_min,
+                    int32_t* host_threads_max) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  int64_t bytes = 0;
+  int32_t lo = 0, hi = 0;
+  for (size_t i = 0; i < g_pool.size(); ++i) {
+    int64_t b = 0;
+    int t = 0;
+    if (nr_scratch_bytes(g_pool[i].ctx.get(), &b) != NR_OK || nr_ctx_get_host_threads(g_pool[i].ctx.get(), &t) != NR_OK)
+      return set_err(NR_ERR_INVALID, "pool inspection failed");
+    bytes += b;
+    lo = i == 0 ? t : std::min(lo, (int32_t)t);
+    hi = i == 0 ? t : std::max(hi, (int32_t)t);
+  }
+  if (n_pooled) *n_pooled = (int64_t)g_pool.size();
+  if (scratch_bytes) *scratch_bytes = bytes;
+  if (host_threads_min) *host_threads_min = lo;
+  if (host_threads_max) *host_threads_max = hi;
+  return NR_OK;
 }
 
 void netrep_DiscardPrefetch(void) {

@@ -7,4 +7,4 @@ rm -f gpurun_out/parity_maxerr.json
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $D/pytest.log 2>&1 && \
 cp gpurun_out/parity_maxerr.json $D/ && \
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.txt 2>&1 && \
-bash tools/runs/r4_stamps.sh r4stamps
+bash profiles/r04/scripts/r4_stamps.sh r4stamps

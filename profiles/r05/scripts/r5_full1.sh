@@ -10,5 +10,5 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $D/pytest_gpu.txt 2>&1
 timeout -k 10 400 python -u bench.py --config C5 --perms-per-step 1024 --steps 1 --warmup 1 --no-cpu-baseline > $D/C5.json 2> $D/C5.err
-bash tools/runs/r5_props.sh
-bash tools/runs/r5_block.sh
+bash tools/props_record.sh
+bash profiles/r05/scripts/r5_block.sh

@@ -64,6 +64,23 @@ def assert_stats_close(got, exp, rtol=RTOL, floor=FLOOR, what=""):
     return float(err.max()) if err.size else 0.0
 
 
+def relative_error_record(got, exp, floor=FLOOR):
+    """The cells the bar measures absolutely (finite, 0 < |expected| < floor):
+    their count and their PURE relative error |got - exp| / |exp| (max, 99.9th
+    percentile, median), beside the largest absolute error there (VERDICT r5
+    item 2: reported next to the scaled error, not a pass/fail bar)."""
+    got = np.asarray(got, dtype=np.float64).ravel()
+    exp = np.asarray(exp, dtype=np.float64).ravel()
+    sel = np.isfinite(exp) & np.isfinite(got) & (np.abs(exp) < floor) & (exp != 0.0)
+    if not sel.any():
+        return {"cells": 0}
+    d = np.abs(got[sel] - exp[sel])
+    rel = d / np.abs(exp[sel])
+    return {"cells": int(sel.sum()), "max_rel": float(rel.max()), "p999_rel": float(np.quantile(rel, 0.999)),
+            "median_rel": float(np.median(rel)), "max_abs": float(d.max()),
+            "min_abs_expected": float(np.abs(exp[sel]).min())}
+
+
 # The north star's "p-values must be identical" (R/pperm.R:138-151): the
 # reference's p-values come from exact counts #(null <= obs) and #(null >= obs)
 # after dropping NA, then permp. The GPU cube with its observed statistics and

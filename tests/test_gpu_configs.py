@@ -33,7 +33,7 @@ from netrep_amd.api import RMatrix
 from oracle import netrep_oracle as O
 from oracle import ref_cpp
 
-from conftest import ROOT, assert_pvalues_identical, assert_stats_close
+from conftest import ROOT, assert_pvalues_identical, assert_stats_close, relative_error_record
 
 pytestmark = pytest.mark.gpu
 
@@ -158,19 +158,21 @@ def test_c3_discovery_vectors_vs_numpy_oracle(c3):
 
 
 def test_c3_nulls_vs_cpp_oracle(c3):
-    """64 permutations x 50 modules of the metric's workload (3,200 summary
-    profiles at S = 500) plus the observed statistics."""
-    seed, p0 = 0x5EED, 123_456
-    got = c3.eng.run(p0, p0 + 64, seed)
-    exp, obs = c3.oracle(p0, p0 + 64, seed, True)
+    """256 permutations x 50 modules of the metric's workload (12,800 summary
+    profiles at S = 500) plus the observed statistics (the CPU restatement
+    takes ~30 s on 16 threads)."""
+    seed, p0, n_perm = 0x5EED, 123_456, 256
+    got = c3.eng.run(p0, p0 + n_perm, seed)
+    exp, obs = c3.oracle(p0, p0 + n_perm, seed, True)
     gobs = c3.eng.observed()
     # the metric's path: the Gram table, chosen from the shapes (the bench times this kernel)
     assert c3.eng.gram_table()
     e1 = assert_stats_close(gobs, obs, what="C3 observed")
     e2 = assert_stats_close(got, exp, what="C3 nulls")
-    record("C3 nulls (64 perms x 50 modules, S=500)", max(e1, e2), perms=64)
+    record(f"C3 nulls ({n_perm} perms x 50 modules, S=500)", max(e1, e2), perms=n_perm,
+           small_cells=relative_error_record(got, exp))
     k = np.diff(c3.node_off)
-    record_pvalues("C3 (64 perms x 50 modules x 7 statistics)",
+    record_pvalues(f"C3 ({n_perm} perms x 50 modules x 7 statistics)",
                    assert_pvalues_identical(got, gobs, exp, obs, k, c3.n, what="C3"))
 
 
@@ -231,7 +233,8 @@ def test_c4_network_only_full_size(c3):
     gobs = c3.eng_nodata.observed()
     e1 = assert_stats_close(gobs, obs, what="C4 observed")
     e2 = assert_stats_close(got, exp, what="C4 nulls")
-    record("C4 nulls (256 perms x 50 modules, network only)", max(e1, e2), perms=256)
+    record("C4 nulls (256 perms x 50 modules, network only)", max(e1, e2), perms=256,
+           small_cells=relative_error_record(got, exp))
     record_pvalues("C4 (256 perms x 50 modules x 4 statistics)",
                    assert_pvalues_identical(got, gobs, exp, obs, np.diff(c3.node_off), c3.n, what="C4"))
 
@@ -246,7 +249,8 @@ def test_c2_exact_shape():
         gobs = c.eng.observed()
         e1 = assert_stats_close(gobs, obs, what="C2 observed")
         e2 = assert_stats_close(got, exp, what="C2 nulls")
-        record("C2 nulls (256 perms x 20 modules, S=100)", max(e1, e2), perms=256)
+        record("C2 nulls (256 perms x 20 modules, S=100)", max(e1, e2), perms=256,
+               small_cells=relative_error_record(got, exp))
         record_pvalues("C2 (256 perms x 20 modules x 7 statistics)",
                        assert_pvalues_identical(got, gobs, exp, obs, np.diff(c.node_off), c.n, what="C2"))
     finally:
@@ -298,6 +302,7 @@ def test_c5_three_datasets_null_all():
         ocv += k * (k - 1) // 2
     errs = []
     pv = []
+    cubes = []
     for t in range(3):
         # test dataset t: all 40,000 genes in a dataset-specific column order;
         # its modules are the discovery modules (mapped through the names)
@@ -332,13 +337,16 @@ def test_c5_three_datasets_null_all():
             np.concatenate([disc["contribution"][m] for m in mods]), n_perm, pi=pis, n_threads=ORACLE_THREADS)
         errs.append(assert_stats_close(res["observed"], obs, what=f"C5 dataset {t} observed"))
         errs.append(assert_stats_close(res["nulls"], exp, what=f"C5 dataset {t} nulls"))
+        cubes.append((res["nulls"], exp))
         # p-values: totalSize = ncol(test) for null = "all" (R/modulePreservation.R:650-654)
         n_vars = np.array([mi.test_idx[m].size if m in mi.test_idx else 0 for m in modules])
         pv.append(assert_pvalues_identical(res["nulls"], res["observed"], exp, obs, n_vars, n,
                                            what=f"C5 dataset {t}"))
         del tcn, tnn, txn
     record("C5 (3 test datasets x 3 perms x 40 modules, null=all, S=1000, k<=2000)", max(errs),
-           datasets=3, perms_per_dataset=3)
+           datasets=3, perms_per_dataset=3,
+           small_cells=relative_error_record(np.concatenate([g.ravel() for g, _ in cubes]),
+                                             np.concatenate([x.ravel() for _, x in cubes])))
     record_pvalues("C5 (3 test datasets x 3 perms x 40 modules x 7 statistics)",
                    {"count_mismatches": sum(r["count_mismatches"] for r in pv),
                     "exact_ties": sum(r["exact_ties"] for r in pv),

@@ -56,6 +56,23 @@ def test_scale_matches_oracle(bundled, bundled_expected):
     assert_stats_close(got, bundled_expected["scaled_test_data"], rtol=1e-13, floor=1.0, what="Scale")
 
 
+@pytest.mark.parametrize("s,n", [(37, 100_003), (1_100_000, 3), (500, 1)])
+def test_scale_column_chunks_match_oracle(s, n):
+    """netrep_Scale streams ~8 MiB column chunks through pinned staging: many
+    chunks with a ragged last one, one column longer than a chunk, a single
+    column. Every column as src/scale.cpp:14-25 (numpy restatement), with a
+    constant column (sd 0: NaN, as the reference gives)."""
+    from oracle import netrep_oracle as O
+    rng = np.random.default_rng(s + n)
+    x = np.asfortranarray(rng.standard_normal((s, n)) * 3.0 + 1.5)
+    x[:, n // 2] = 2.0
+    got = N.Scale(RMatrix(x)).values
+    exp = O.scale(x)
+    # the north-star bar (a 1.1M-long column's sum rounds differently in
+    # the kernel's 64 lane sums than in numpy's pairwise sum)
+    assert_stats_close(got, exp, rtol=1e-10, floor=1.0, what=f"Scale {s}x{n}")
+
+
 def test_check_finite():
     N.CheckFinite(np.ones((4, 3)))
     bad = np.ones((4, 3))

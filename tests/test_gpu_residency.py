@@ -208,13 +208,53 @@ def test_cancel_after_run_does_not_stick_to_a_cleared_context():
         eng.close()
 
 
-def test_pooled_context_host_threads_back_to_default():
-    """a pooled context returns to the process default host-thread
-    count, whatever nCores the call that used it passed."""
+def _pool_info():
+    import ctypes as C
+    from netrep_amd import _lib as L
+    n, b = C.c_int64(), C.c_int64()
+    lo, hi = C.c_int32(), C.c_int32()
+    assert L.load().netrep_PoolInfo(C.byref(n), C.byref(b), C.byref(lo), C.byref(hi)) == L.NR_OK
+    return n.value, b.value, lo.value, hi.value
+
+
+@pytest.mark.parametrize("n_cores", [3, 16])
+def test_pooled_context_host_threads_back_to_default(n_cores):
+    """a PermutationProcedure call with nCores different from
+    the process default sets its contexts' host threads to nCores; once the
+    call returns, every pooled context is back at the default
+    (nr_get_host_threads) and holds no per-batch work buffers (its column-sweep
+    sets and slot scratch are released with its dataset)."""
     from netrep_amd import _lib as L
     lib = L.load()
     default = lib.nr_get_host_threads()
-    assert 1 <= default <= 16
+    assert 1 <= default <= 16 and default != n_cores
+    N.ReleaseResident()
+    lay, names, ma, x, c, nt = _dataset(n=1200, s=60, seed=91, sizes=(100, 50, 20))
+    disc = N.IntermediatePropertiesNoData(RMatrix(c, names, names), RMatrix(nt, names, names), names, ma,
+                                          lay.modules)
+    out = N.PermutationProcedureNoData(disc, RMatrix(c, names, names), RMatrix(nt, names, names), ma,
+                                       lay.modules, 64, nCores=n_cores, seed=3)
+    assert out["nulls"].shape[-1] == 64
+    n_pooled, scratch, lo, hi = _pool_info()
+    assert n_pooled >= 1
+    assert lo == hi == default, (lo, hi, default)
+    assert scratch == 0, scratch
+    N.ReleaseResident()
+    assert _pool_info()[0] == 0
+
+
+def test_peer_staged_pairs_zero_on_one_device():
+    """Contexts on one GPU never need peer copies: no pair is recorded as
+    host-staged by a broadcast between them."""
+    import ctypes as C
+    from netrep_amd import _lib as L
+    lay, names, ma, x, c, nt = _dataset(n=700, s=30, seed=93, sizes=(60, 20))
+    with N.Engine(0) as a, N.Engine(0) as b:
+        a.set_dataset(c, nt, None)
+        a.broadcast_dataset_to([b])
+    n = C.c_int(-1)
+    assert L.load().nr_peer_staged_pairs(C.byref(n)) == L.NR_OK
+    assert n.value == 0
 
 
 @pytest.mark.skipif(N.device_count() < 2, reason="needs two physical GPUs")
