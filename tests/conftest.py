@@ -9,6 +9,40 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, ROOT)
 
 
+# Largest scaled error of every full-size parity case, written to
+# gpurun_out/parity_maxerr.json at the end of the session (the record quoted in
+# DESIGN.md); entries of earlier sessions are kept unless overwritten.
+REPORT = {}
+
+
+def record(name, err, **extra):
+    REPORT[name] = dict(max_scaled_error=err, **extra)
+    print(f"{name}: max scaled error {err:.3e} {extra}")
+
+
+def record_pvalues(name, rec):
+    REPORT["p-values: " + name] = rec
+    print(f"p-values {name}: {rec}")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _parity_report():
+    yield
+    if not REPORT:
+        return
+    import json
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    path = os.path.join(out, "parity_maxerr.json")
+    old = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f)
+    old.update(REPORT)
+    with open(path, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP engine)")
 

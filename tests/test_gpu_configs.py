@@ -21,9 +21,6 @@ bit for bit (conftest.assert_stats_close).
 The largest scaled error of every case is written to
 gpurun_out/parity_maxerr.json (the record quoted in DESIGN.md).
 """
-import json
-import os
-
 import numpy as np
 import pytest
 
@@ -33,37 +30,11 @@ from netrep_amd.api import RMatrix
 from oracle import netrep_oracle as O
 from oracle import ref_cpp
 
-from conftest import ROOT, assert_pvalues_identical, assert_stats_close, relative_error_record
+from conftest import assert_pvalues_identical, assert_stats_close, record, record_pvalues, relative_error_record
 
 pytestmark = pytest.mark.gpu
 
 ORACLE_THREADS = 16
-REPORT = {}
-
-
-@pytest.fixture(scope="module", autouse=True)
-def _report():
-    yield
-    out = os.path.join(ROOT, "gpurun_out")
-    os.makedirs(out, exist_ok=True)
-    path = os.path.join(out, "parity_maxerr.json")
-    old = {}
-    if os.path.exists(path):
-        with open(path) as f:
-            old = json.load(f)
-    old.update(REPORT)
-    with open(path, "w") as f:
-        json.dump(old, f, indent=1, sort_keys=True)
-
-
-def record(name, err, **extra):
-    REPORT[name] = dict(max_scaled_error=err, **extra)
-    print(f"{name}: max scaled error {err:.3e} {extra}")
-
-
-def record_pvalues(name, rec):
-    REPORT["p-values: " + name] = rec
-    print(f"p-values {name}: {rec}")
 
 
 def _torch():

@@ -23,8 +23,7 @@ from netrep_amd import synthetic as S
 from oracle import netrep_oracle as O
 from oracle import ref_cpp
 
-from conftest import assert_stats_close, relative_error_record
-from test_gpu_configs import record
+from conftest import assert_stats_close, record, relative_error_record
 
 pytestmark = pytest.mark.gpu
 
