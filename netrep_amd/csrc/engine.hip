@@ -302,7 +302,6 @@ struct ProfilePlan {
   bool big = false;   // modules beyond kvec (per-node arrays in scratch)
   int64_t basis_doubles = 0;
   int64_t g32_off = 0;  // fp32 Gram copy (relaxed Lanczos steps), 0: none
-  int64_t c16_off = 0;  // its 16-bit corrections (Gram-table launches: the six-byte tier), 0: none
 };
 
 // Queue order of the summary-profile items. Module-major (every permutation
@@ -513,13 +512,6 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
                             nr::fused_net_fits(nr::kPackedLayoutK, std::min(nr::kPackedLayoutK, 160), nr::kTableWaves);
     fuse_kind[i] = fuse_table ? 1 : 0;
     fuse[i] = fuse_kind[i] != 0;
-    if (fuse_table && seg[i].plan.g32_off > 0) {
-      // the six-byte tier of the table kernel's Lanczos matvecs (kernels.hip
-      // c16_encode): 2 bytes per packed entry behind the fp32 copy
-      ProfilePlan& pl = seg[i].plan;
-      pl.c16_off = pl.stride;
-      pl.stride += (pl.gram_doubles / 4 + 31) / 32 * 32;
-    }
     total = std::max<int64_t>(total, seg[i].plan.stride * seg[i].plan.slots);
   }
   // segments run one after the other on one stream: they share the scratch
@@ -542,7 +534,6 @@ int launch_profiles(nr_ctx* ctx, nr::ProfileParams pp, const int32_t* d_order,
     pp.order_tail =
         profile_order_tail(plan.slots, k_sorted, seg[i].first, seg[i].count, n_perm, (int)pp.n_samples);
     pp.g32_off = plan.g32_off;
-    pp.c16_off = plan.c16_off;
     pp.fused = fuse_kind[i];
     if (pp.fused) {
       pp.net = *table_np;

@@ -100,8 +100,6 @@ struct ProfileParams {
   int64_t basis_doubles;       // Lanczos basis doubles per slot (behind the Gram)
   int64_t g32_off;             // doubles from the slot start to the fp32 copy of the packed Gram
                                // (relaxed Lanczos steps; 0: no copy, fp64 matvecs throughout)
-  int64_t c16_off;             // doubles from the slot start to the int16 corrections of the fp32
-                               // copy (the six-byte tier of the Gram-table kernel; 0: none)
   int32_t vec_global;          // 1: the Lanczos vectors, per-node arrays and index set in the slot's
                                // scratch too (Lanczos dimensions beyond the LDS vectors: variant 6)
   int32_t order_tail;          // queue order: 0 = module-major (large modules first); T > 0 =

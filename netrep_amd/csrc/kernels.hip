@@ -283,36 +283,16 @@ __device__ __forceinline__ int64_t pk_at(int r, int c, int kc) {  // r >= 16 (c 
 }
 __device__ __forceinline__ int64_t pk_col(int c, int kc) { return pk_at(c, c, kc); }  // the diagonal G_cc
 
-// The six-byte tier of the packed Gram: the fp32 copy f of an entry g plus
-// c = rint((g - f) / ulp(f) * 2^15) in 16 bits (|g - f| <= ulp(f) / 2, so
-// |c| <= 2^14), with ulp(f) = 2^(e - 24) for f = m 2^e, m in [0.5, 1): the
-// pair carries g to ~2^-39 relative per entry, read as f + c 2^(e - 39).
-// (Entries below fp32's normal range clamp; the matvec error they add is
-// absolute, ~1e-38, far below the Gram's norm.)
-__device__ __forceinline__ short c16_encode(double g, float f) {
-  const double c = rint(__builtin_amdgcn_ldexp(g - (double)f, 39 - __builtin_amdgcn_frexp_expf(f)));
-  return (short)fmin(32767.0, fmax(-32767.0, __builtin_isfinite(c) ? c : 0.0));
-}
-__device__ __forceinline__ double c16_decode(float f, int c) {
-  return (double)f + __builtin_amdgcn_ldexp((double)c, __builtin_amdgcn_frexp_expf(f) - 39);
-}
-
 // Where a Gram-table item puts its Gram: the slot's packed Gram (and its fp32
-// copy, and the copy's corrections) of side kc = k + 1, the ones column's
-// entries from colsum, and S.
+// copy) of side kc = k + 1, the ones column's entries from colsum, and S.
 struct GramOut {
   double* G;
   float* G32;
-  short* C16;
   int kc;
   double S;
   __device__ __forceinline__ void put(int64_t a, double v) const {
     G[a] = v;
-    if (G32) {
-      const float f = (float)v;
-      G32[a] = f;
-      if (C16) C16[a] = c16_encode(v, f);
-    }
+    if (G32) G32[a] = (float)v;
   }
 };
 
@@ -1239,21 +1219,16 @@ __device__ void gram_mfma_dual(const double* __restrict__ X, int S, const uint32
 //
 // SQ: out_r = sum_c G_rc^2 over c < k instead (squared row norms of the
 // leading k x k block, for start_column; x and y unused).
-// C6 (with F32): the six-byte tier, each fp32 entry corrected by its 16-bit
-// c16 (c16_decode); G is the fp32 copy and C16 the corrections, same layout.
-template <int NW, bool F32 = false, bool SQ = false, bool C6 = false>
+template <int NW, bool F32 = false, bool SQ = false>
 __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int kc, int k, const double* x,
                                                  double* out, double* part, int ks,
-                                                 const double* y, double* red, const short* C16 = nullptr) {
-  static_assert(!C6 || F32, "the six-byte tier corrects the fp32 copy");
+                                                 const double* y, double* red) {
   constexpr int EB = F32 ? 4 : 8;  // element bytes
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = kc;  // rows of the packed layout
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, (int)(pk_base(pk_groups(kc), P) * EB),
                                                       0x00020000);
-  const auto csrc = __builtin_amdgcn_make_buffer_rsrc((void*)C16, (short)0,
-                                                      C6 ? (int)(pk_base(pk_groups(kc), P) * 2) : 0, 0x00020000);
   const int ncg = (k + 15) / 16;
   int n_units = 0;
   for (int g = 0; g < ncg; ++g) n_units += (P - 16 * g + 63) >> 6;
@@ -1273,13 +1248,10 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
   // loads (32 per lane) before the first wait; the matvec is latency-bound at
   // three workgroups per CU, not byte-bound (profiles/r02/profile_variants.txt).
   // A unit beyond the wave's range loads nothing (range-checked offsets).
-  // The six-byte tier: one unit in flight (its 16 fp32 and 16 correction
-  // registers take the place of one fp64 unit's 32).
-  constexpr int UF = C6 ? 1 : (F32 ? 2 : NR_MV_UF64);
+  constexpr int UF = F32 ? 2 : NR_MV_UF64;
   using LT = typename std::conditional<F32, float, double>::type;
   for (int u = u0; u < u1; u += UF) {
     LT gb[UF][16];
-    int gc[C6 ? UF : 1][16];
     {
       int lcg = cg, lj = j;
 #pragma unroll
@@ -1289,8 +1261,6 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
         const int64_t base = pk_base(lcg, P) + 1024 * (int64_t)lj;
         const int vo = valid && lane < h ? lane * EB : (int)0x80000000;
         int so = valid ? (int)base * EB : 0;
-        const int co = valid && lane < h ? lane * 2 : (int)0x80000000;
-        int sc = valid ? (int)base * 2 : 0;
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
           if (F32)
@@ -1298,10 +1268,6 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
           else
             gb[i][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, so, 0));
           so += h * EB;
-          if constexpr (C6) {
-            gc[i][t] = (int)(short)__builtin_amdgcn_raw_buffer_load_b16(csrc, co, sc, 0);
-            sc += h * 2;
-          }
         }
         if (++lj == ((P - 16 * lcg + 63) >> 6)) {
           ++lcg;
@@ -1331,11 +1297,7 @@ __device__ __forceinline__ double packed_matvec(const void* __restrict__ G, int 
         const double xl = c0 + (lane & 15) < k ? x[c0 + (lane & 15)] : 0.0;  // the unit's 16 x_c, one per lane
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-          double gt;
-          if constexpr (C6)
-            gt = c16_decode((float)gb[i][t], gc[i][t]);
-          else
-            gt = (double)gb[i][t];
+          const double gt = (double)gb[i][t];
           acc += gt * nr_readlane_f64(xl, t);  // (saves 30 VGPRs over 16 LDS reads)
           up[t] += (!diag || r > c0 + t) ? gt * xr : 0.0;
         }
@@ -1600,21 +1562,13 @@ __device__ __forceinline__ void ritz_vector_wave(const double* __restrict__ Q, i
 // accuracy: the later a step, the smaller its weight in the Ritz vector;
 // offline study on C3 null items, tools/sim_lanczos_relax.py: same steps, same
 // 2e-14 worst eigenvector error as fp64 throughout, 19% fewer Gram bytes).
-// *relax is the matvec tier: 0 fp64, 2 the fp32 copy; with tier6 (round 6,
-// the Gram-table kernel) tier 1, the fp32 copy plus its 16-bit corrections
-// (~2^-39 relative per entry, 6 bytes), from the first check whose residual
-// is below kTier6 theta on, and the first check comes at step 8 so that the
-// switch can happen early (offline, tools/sim_lanczos_tier6.py, C3 null
-// items: Gram bytes per entry 201.8 -> 181.3, worst eigenvector error
-// 1.2e-14 against 1.6e-14 for the two tiers).
 // q_given: start from the vector the caller left in L.q (start_column's
 // G e_c*) instead of the near-constant one. gv_out: also leave G v in L.gv,
 // from the Lanczos relation (see the end of the function).
-constexpr double kTier6 = 1e-3;
 template <int NW, bool BF, class MV>
 __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, const LzLds& L, int* flags,
-                                             double* Q, MV& mv, uint64_t& t_mark, int* relax = nullptr,
-                                             bool q_given = false, bool gv_out = false, bool tier6 = false) {
+                                             double* Q, MV& mv, uint64_t& t_mark, bool* relax = nullptr,
+                                             bool q_given = false, bool gv_out = false) {
   constexpr int BS = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mmax = L.mmax;
@@ -1658,7 +1612,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   // check's Sturm passes in full; C2 shape 1.908 -> 1.841 ms per 256
   // permutations, 0.02% more steps. The 4-wave kernels keep 16: at C3, 20
   // and 24 measured -0.2% and +0.9%, profiles/r05/firstcheck/)
-  const int first_check = NW == 1 ? 20 : (tier6 ? 8 : 16);
+  constexpr int first_check = NW == 1 ? 20 : 16;
   int next_check = mcap < first_check ? mcap : first_check;
   int prev_j = 0;  // lane 0 of wave 0 only
   double prev_r = 0.0;
@@ -1669,7 +1623,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   if (tid == 0) {
     omg[0] = 1.0;  // omega_{0,0}
     s_reorth = 0;
-    flags[5] = 0;  // matvec tier (0 fp64, 1 six-byte, 2 fp32)
+    flags[5] = 0;  // relaxed (fp32) matvecs
   }
   for (int c = tid; c < k; c += BS) Q[c] = q[c];  // q_0 (later q_j are stored by the update below)
   for (int j = 0; j < mcap; ++j) {
@@ -1741,8 +1695,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
           const double tol = NR_LZ_TOL * fabs(theta);
           const bool conv = resid <= tol;
           s_done = conv || last || !(beta_j > 1e-300 * fabs(theta));
-          if (relax && tier6 && flags[5] == 0 && resid <= kTier6 * fabs(theta)) flags[5] = 1;
-          if (relax && resid <= 1e-7 * fabs(theta)) flags[5] = 2;
+          if (relax && resid <= 1e-7 * fabs(theta)) flags[5] = 1;
           // the Ritz vector's coefficients: inverse iteration (LU), once
           if (s_done) {
             NR_STAMP(7);
@@ -1760,21 +1713,6 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
             const double need = ceil(log(tol / resid) / rate);
             step = need < 1.0 ? 1 : (need > 8.0 ? 8 : (int)need);
           }
-          // Still on fp64 matvecs: also check where the decay predicts the
-          // residual's crossing of the fp32 threshold (the decay since the
-          // previous check, or since step 0 at residual theta for the first),
-          // so the relaxed phase starts near the crossing instead of at the
-          // next convergence check. Offline (tools/sim_lanczos_tiers.py, C3
-          // null items): Gram bytes per entry 226.8 -> 216.6, +0.25 checks.
-          // With tier6, the crossing of kTier6 theta too while still on fp64.
-          if (relax && flags[5] < 2 && resid > 1e-7 * fabs(theta) && resid < fabs(theta)) {
-            const double rate = prev_j > 0 && resid < prev_r && resid > 0.0
-                                    ? log(resid / prev_r) / (double)(j + 1 - prev_j)
-                                    : log(resid / fabs(theta)) / (double)(j + 1);
-            const double thr = tier6 && flags[5] == 0 ? kTier6 : 1e-7;
-            const double cross = ceil(log(thr * fabs(theta) / resid) / rate);
-            if (cross >= 1.0 && cross < (double)step) step = (int)cross;
-          }
           prev_j = j + 1;
           prev_r = resid;
           s_next_check = min(j + 1 + step, mcap);
@@ -1783,7 +1721,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       nr_sync<NW>();
       if (s_done) break;
       next_check = s_next_check;
-      if (relax) *relax = flags[5];
+      if (relax) *relax = flags[5] != 0;
       NR_STAMP(7);  // Lanczos: Ritz checks
     }
   }
@@ -1878,8 +1816,6 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
   const int tid = threadIdx.x;
   // fp32 copy of the packed Gram for the relaxed Lanczos steps (0: off)
   float* G32 = PACKED && P.g32_off > 0 ? reinterpret_cast<float*>(G + P.g32_off) : nullptr;
-  // its 16-bit corrections (the six-byte tier; Gram-table launches only)
-  short* C16 = TABLE && G32 && P.c16_off > 0 ? reinterpret_cast<short*>(G + P.c16_off) : nullptr;
   if (pglob) part = Q + P.basis_doubles;
   // modules of more than kmax nodes (dual by construction, engine.hip
   // plan_profile): x_c.u, column means, sums of squares, contributions and the
@@ -1919,7 +1855,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       // a zeroed region: padding and the diagonal blocks' upper parts stay 0)
       // and the matrix-core Gram is skipped. The per-node arrays live in the
       // Lanczos vectors' LDS, idle until the Lanczos phase.
-      const GramOut go{G, G32, C16, kc, Sd};
+      const GramOut go{G, G32, kc, Sd};
       {
         // The fill below writes every lower-triangle entry over kc = k + 1
         // (pairs, diagonal, ones column); zero only what it never writes: the
@@ -1969,20 +1905,17 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       if (!dual)
         for (int c = tid; c < k; c += BS)
           L.colm[c] = (PACKED ? gl(pk_at(k, c, kc)) : G[k + (int64_t)c * ld]) / Sd;
-      int relax = 0;  // matvec tier (lanczos_ritz)
+      bool relax = false;
       auto mv = [&](const double* x, double* out, const double* y) -> double {
         if (!PACKED) return matvec(G, ld, n, x, out, part, kmax, y, L.red);
-        if (TABLE && relax == 1)
-          return packed_matvec<NW, true, false, true>(G32, kc, n, x, out, part, kmax, y, L.red, C16);
         return relax ? packed_matvec<NW, true, false>(G32, kc, n, x, out, part, kmax, y, L.red)
                      : packed_matvec<NW, false, false>(G, kc, n, x, out, part, kmax, y, L.red);
       };
       const bool q_given = PACKED && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
       NR_STAMP(8);  // start column
       const bool gv_rel = !dual;
-      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel,
-                               C16 != nullptr);
-      relax = 0;  // node contributions: the fp64 Gram
+      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel);
+      relax = false;  // node contributions: the fp64 Gram
       if (!TABLE && dual) {
         profile_contrib_dual<NW>(P, k, m, Li, X, S, g1[0]);
       } else {
