@@ -124,62 +124,87 @@ __device__ __forceinline__ double nr_rcp(double d) {
 // counts use the characteristic-polynomial recurrence of the Gershgorin-
 // normalised matrix, p_i = (a_i - x) p_{i-1} - b_{i-1}^2 p_{i-2} (sign changes
 // of p_0..p_n = eigenvalues below x): one FMA on the dependency chain per
-// step and no division; |p| is renormalised every 4 steps.
+// step and no division; |p| is renormalised every 4 steps. Each pass puts
+// lane l's point at lo + (hi - lo) (l + 1) / 64 (lane 63 on hi, an upper
+// bound already counted: the division by 64 is exact, no divide on the wave's
+// path) and keeps the one-64th subinterval the counts bracket.
 //
-// Warm start (r_prev > 0): theta_prev, the top Ritz value of an earlier
-// check, is a lower bound (Cauchy interlacing), and its Ritz residual r_prev
-// bounds the distance to an eigenvalue of the grown matrix, so the top one
-// lies in [theta_prev, theta_prev + r_prev] unless the first pass -- whose
-// last lane sits exactly on that upper end -- finds eigenvalues above it;
-// then the search continues to the Gershgorin bound. Near convergence this
-// halves the passes of a check.
+// Warm start (r_prev > 0): theta_lo, a lower end of an earlier check's
+// bracket of the top Ritz value, is a lower bound (Cauchy interlacing), and
+// its Ritz residual r_prev bounds the distance to an eigenvalue of the grown
+// matrix, so the top one lies in [theta_lo, theta_lo + 1.01 r_prev] unless
+// the first pass finds eigenvalues above it; then the search continues to the
+// Gershgorin bound.
 //
-// wa, wb (n doubles of LDS each, or NULL): the normalised recurrence
-// coefficients alpha_i / scale and (beta_i / scale)^2, computed once per call
-// by the wave instead of in every pass (the passes are issue-bound: three
-// fewer instructions per step; the same products, so the same counts).
-static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha, const double* beta, int n, int lane,
-                                                            double theta_prev = 0.0, double r_prev = 0.0,
-                                                            double* wa = nullptr, double* wb = nullptr) {
+// Two stages (round 6): sturm_init (bounds, warm bracket, the normalised
+// coefficients) and sturm_passes(width) narrowing the bracket to `width`; a
+// Ritz check first narrows to 1e-9 of the scale, which is all its residual
+// estimate needs (tri_top_resid's relative error is O(bracket / gap of T), not
+// O(bracket / residual)), and goes on to 2e-16 only where the run may stop
+// (lanczos_ritz).
+//
+// wa, wb (n doubles of LDS each): the normalised recurrence coefficients
+// alpha_i / scale and (beta_i / scale)^2, computed once by the wave instead
+// of in every pass (the passes are issue-bound).
+struct SturmBracket {
+  double lo, hi, g_hi, scale, inv;
+  bool warm;
+  int passes;
+};
+
+static __device__ __forceinline__ void sturm_coeffs(const double* alpha, const double* beta, int n, int lane,
+                                                    double inv, double* wa, double* wb) {
+  for (int i = lane; i < n; i += 64) {
+    wa[i] = alpha[i] * inv;
+    if (i < n - 1) {
+      const double b = beta[i] * inv;
+      wb[i] = b * b;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+static __device__ __forceinline__ SturmBracket sturm_init(const double* alpha, const double* beta, int n, int lane,
+                                                          double theta_lo, double r_prev, double* wa, double* wb) {
   double lo = alpha[0], hi = alpha[0];
   for (int i = lane; i < n; i += 64) {
     const double r = (i > 0 ? fabs(beta[i - 1]) : 0.0) + (i < n - 1 ? fabs(beta[i]) : 0.0);
     lo = fmin(lo, alpha[i] - r);
     hi = fmax(hi, alpha[i] + r);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  lo = -nr_wave_max(-lo);  // register butterflies (DPP, permlane), no LDS round trips
+  hi = nr_wave_max(hi);
+  SturmBracket b;
+  b.scale = fmax(fabs(lo), fabs(hi)) + 1e-300;
+  b.inv = 1.0 / b.scale;
+  lo -= 1e-14 * b.scale;
+  hi += 1e-14 * b.scale;
+  b.g_hi = hi;
+  b.warm = r_prev > 0.0 && isfinite(r_prev) && theta_lo - 4e-16 * b.scale > lo &&
+           theta_lo + 1.01 * r_prev + 4e-16 * b.scale < hi;
+  if (b.warm) {
+    lo = theta_lo - 4e-16 * b.scale;
+    hi = theta_lo + 1.01 * r_prev + 4e-16 * b.scale;
   }
-  const double scale = fmax(fabs(lo), fabs(hi)) + 1e-300;
-  const double inv = 1.0 / scale;
-  lo -= 1e-14 * scale;
-  hi += 1e-14 * scale;
-  const double g_hi = hi;
-  bool warm = r_prev > 0.0 && isfinite(r_prev) && theta_prev - 4e-16 * scale > lo &&
-              theta_prev + 1.01 * r_prev + 4e-16 * scale < hi;
-  if (warm) {
-    lo = theta_prev - 4e-16 * scale;
-    hi = theta_prev + 1.01 * r_prev + 4e-16 * scale;
-  }
-  if (wa) {
-    for (int i = lane; i < n; i += 64) {
-      wa[i] = alpha[i] * inv;
-      if (i < n - 1) {
-        const double b = beta[i] * inv;
-        wb[i] = b * b;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  for (int it = 0; it < 14; ++it) {
-    // warm first pass: 64 points ending on hi; otherwise 64 interior points
-    const double den = warm ? 64.0 : 65.0;
-    const double x = (lo + (hi - lo) * (double)(lane + 1) / den) * inv;
-    double p0 = 1.0, p1 = alpha[0] * inv - x;
+  b.lo = lo;
+  b.hi = hi;
+  b.passes = 0;
+  sturm_coeffs(alpha, beta, n, lane, b.inv, wa, wb);
+  return b;
+}
+
+static __device__ __forceinline__ void sturm_passes(SturmBracket& b, int n, int lane, const double* wa,
+                                                    const double* wb, double width) {
+  double lo = b.lo, hi = b.hi;
+  const double inv = b.inv;
+  const double frac = (double)(lane + 1) * 0.015625;  // (lane + 1) / 64, exact
+  // (a warm bracket takes one pass whatever its width: that pass checks it)
+  while (b.passes < 16 && (hi - lo > width || b.warm)) {
+    ++b.passes;
+    const double x = (lo + (hi - lo) * frac) * inv;
+    double p0 = 1.0, p1 = wa[0] - x;
     int cnt = p1 < 0.0;  // eigenvalues < x
     // a sign change between p_{i-1} and p_i: the sign bits differ
     auto step = [&](double a, double bb) {
@@ -196,22 +221,14 @@ static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha,
     };
     // 8 steps' coefficients read ahead of their recurrence steps, so the LDS
     // latency is paid once per 8 steps instead of on the dependency chain of
-    // every step (same arithmetic in the same order); whole groups of 8 carry
-    // no per-step bounds test (a single wave pays an issue slot for each)
+    // every step; whole groups of 8 carry no per-step bounds test
     int i0 = 1;
     for (; i0 + 8 <= n; i0 += 8) {
       double av[8], bv[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        const int i = i0 + t;
-        if (wa) {
-          av[t] = wa[i];
-          bv[t] = wb[i - 1];
-        } else {
-          av[t] = alpha[i] * inv;
-          const double b = beta[i - 1] * inv;
-          bv[t] = b * b;
-        }
+        av[t] = wa[i0 + t];
+        bv[t] = wb[i0 + t - 1];
       }
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -220,36 +237,25 @@ static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha,
       }
     }
     for (int i = i0; i < n; ++i) {
-      double a, bb;
-      if (wa) {
-        a = wa[i];
-        bb = wb[i - 1];
-      } else {
-        a = alpha[i] * inv;
-        const double b = beta[i - 1] * inv;
-        bb = b * b;
-      }
-      step(a, bb);
+      step(wa[i], wb[i - 1]);
       if ((i & 3) == 0) renorm();
     }
-    // largest x with cnt <= n-1 becomes lo; smallest x with cnt == n becomes hi
-    const unsigned long long below = __ballot(cnt <= n - 1);
     // lanes are ordered by x: lanes [0, t) have cnt <= n-1, lanes [t, 64) have cnt == n
-    const int t = __popcll(below);
-    if (warm && t == 64) {  // eigenvalues above the residual bound: cold search above it
+    const int t = __popcll(__ballot(cnt <= n - 1));
+    if (t == 64) {  // eigenvalues above the bracket (a warm start's residual bound): search above it
       lo = hi;
-      hi = g_hi;
-      warm = false;
+      hi = b.g_hi;
+      b.warm = false;
       continue;
     }
-    const double xlo = lo + (hi - lo) * (double)t / den;
-    const double xhi = lo + (hi - lo) * (double)(t + 1) / den;
+    const double xlo = lo + (hi - lo) * ((double)t * 0.015625);
+    const double xhi = lo + (hi - lo) * ((double)(t + 1) * 0.015625);
     lo = xlo;
     hi = xhi;
-    warm = false;
-    if (hi - lo <= 2e-16 * scale) break;
+    b.warm = false;
   }
-  return 0.5 * (lo + hi);
+  b.lo = lo;
+  b.hi = hi;
 }
 
 // Convergence estimate of the top Ritz pair: |last component| of the unit
@@ -257,15 +263,18 @@ static __device__ __forceinline__ double tri_top_eigenvalue(const double* alpha,
 // three-term recurrence run BACKWARDS from y_{n-1} = 1: the top eigenvector
 // of an unreduced Jacobi matrix is positive and its tail decays once the
 // pair converges, so upward it is the dominant (stable) solution. rb holds
-// 1/beta[0..n-1), one wave fills it. Returns beta_j / |y| (lane 0).
-static __device__ __forceinline__ double tri_top_resid(const double* alpha, const double* beta, int n, double theta, double beta_j,
-                                double* rb, int lane) {
+// 1/beta[0..n-1), one wave fills it. Returns beta_j / |y| (every lane). The
+// recurrence reads its coefficients eight steps ahead (round 6: the LDS
+// latency off the dependency chain; the same arithmetic in the same order).
+static __device__ __forceinline__ double tri_top_resid(const double* alpha, const double* beta, int n, double theta,
+                                                       double beta_j, double* rb, int lane) {
   for (int i = lane; i < n - 1; i += 64) rb[i] = 1.0 / beta[i];
-  __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   double y1 = 1.0, y2 = 0.0, ss = 1.0;  // y_i, y_{i+1}, sum of squares
-  for (int i = n - 1; i > 0; --i) {
-    const double y0 = fma(theta - alpha[i], y1, -(i < n - 1 ? beta[i] : 0.0) * y2) * rb[i - 1];
+  auto step = [&](double a, double b, double r) {
+    const double y0 = fma(theta - a, y1, -b * y2) * r;
     ss = fma(y0, y0, ss);
     y2 = y1;
     y1 = y0;
@@ -275,8 +284,30 @@ static __device__ __forceinline__ double tri_top_resid(const double* alpha, cons
       ss *= 1e-200;
       beta_j *= 1e-100;
     }
+  };
+  int i = n - 1;
+  for (; i >= 8; i -= 8) {  // steps i .. i - 7, all >= 1
+    double av[8], bv[8], rv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      av[t] = alpha[i - t];
+      bv[t] = i - t < n - 1 ? beta[i - t] : 0.0;
+      rv[t] = rb[i - t - 1];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) step(av[t], bv[t], rv[t]);
   }
+  for (; i > 0; --i) step(alpha[i], i < n - 1 ? beta[i] : 0.0, rb[i - 1]);
   return beta_j / sqrt(ss);
+}
+
+// log2 of a positive double for the Ritz checks' step predictions: exponent
+// plus the fp32 log2 of the mantissa (v_log_f32), ~1e-7 absolute; the library
+// log's ~40 dependent instructions sat on lane 0 of a check's serial path.
+static __device__ __forceinline__ double nr_log2_fast(double x) {
+  const int e = __builtin_amdgcn_frexp_exp(x);
+  const float m = (float)__builtin_amdgcn_frexp_mant(x);
+  return (double)e + (double)__builtin_amdgcn_logf(m);
 }
 
 // Eigenvector of the tridiagonal for eigenvalue theta by two steps of inverse

@@ -1687,9 +1687,23 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     const bool last = (j + 1 == mcap);
     if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
       if (wave == 0) {
-        const double theta = tri_top_eigenvalue(alpha, beta, j + 1, lane, hint_theta, hint_r, h, ty);  // h, ty idle here
-        const double resid = tri_top_resid(alpha, beta, j + 1, theta, beta_j, ty, lane);
-        hint_theta = theta;
+        // the top eigenvalue to 1e-9 of the scale, enough for the residual
+        // estimate; to 2e-16 where the run may stop here (its Ritz pair is
+        // then the result)
+        SturmBracket sb = sturm_init(alpha, beta, j + 1, lane, hint_theta, hint_r, h, ty);  // h, ty idle here
+        sturm_passes(sb, j + 1, lane, h, ty, 1e-9 * sb.scale);
+        double theta = 0.5 * (sb.lo + sb.hi);
+        NR_STAMP(13);  // Ritz check: the top eigenvalue (Sturm multisection)
+        double resid = tri_top_resid(alpha, beta, j + 1, theta, beta_j, ty, lane);
+        if ((resid <= 1e3 * NR_LZ_TOL * fabs(theta) || last || !(beta_j > 1e-300 * fabs(theta))) &&
+            sb.hi - sb.lo > 2e-16 * sb.scale) {
+          sturm_coeffs(alpha, beta, j + 1, lane, sb.inv, h, ty);  // ty held the residual's reciprocals
+          sturm_passes(sb, j + 1, lane, h, ty, 2e-16 * sb.scale);
+          theta = 0.5 * (sb.lo + sb.hi);
+          resid = tri_top_resid(alpha, beta, j + 1, theta, beta_j, ty, lane);
+        }
+        NR_STAMP(14);  // Ritz check: the residual (backward recurrence)
+        hint_theta = sb.lo;  // a lower bound of the top eigenvalue (the next check's warm start)
         hint_r = resid;
         if (lane == 0) {
           const double tol = NR_LZ_TOL * fabs(theta);
@@ -1709,8 +1723,9 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
           if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
           int step = 8;
           if (prev_j > 0 && resid < prev_r && resid > 0.0) {
-            const double rate = log(resid / prev_r) / (double)(j + 1 - prev_j);  // < 0
-            const double need = ceil(log(tol / resid) / rate);
+            const double lr = nr_log2_fast(resid);
+            const double rate = (lr - nr_log2_fast(prev_r)) / (double)(j + 1 - prev_j);  // < 0
+            const double need = ceil((nr_log2_fast(tol) - lr) / rate);
             step = need < 1.0 ? 1 : (need > 8.0 ? 8 : (int)need);
           }
           prev_j = j + 1;

@@ -28,7 +28,7 @@ def _ptr(a, ctype=C.c_double):
 # The 16 phase-stamp slots as include/netrep_gpu.h (nr_set_stamps) lists them.
 STAMP_SLOTS = ["index", "gram", "lanczos_setup", "matvec", "three_term_omega", "statistics", "q_update",
                "ritz_checks", "start_column", "reorth", "ritz_vector", "node_contributions", "ritz_coefficients",
-               "s13", "s14", "s15"]
+               "check_eigenvalue", "check_residual", "s15"]
 
 
 class Engine:
