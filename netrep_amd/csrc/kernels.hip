@@ -1624,6 +1624,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     omg[0] = 1.0;  // omega_{0,0}
     s_reorth = 0;
     flags[5] = 0;  // relaxed (fp32) matvecs
+    // the next check is predicted to end the run: its eigenvalue to full
+    // precision in one go (the wave class's first check, at step 20, usually
+    // does: C2 items stop at ~24 steps)
+    flags[6] = NW == 1;
   }
   for (int c = tid; c < k; c += BS) Q[c] = q[c];  // q_0 (later q_j are stored by the update below)
   for (int j = 0; j < mcap; ++j) {
@@ -1688,14 +1692,15 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     if (j + 1 == next_check || last || !(beta_j > 1e-300)) {
       if (wave == 0) {
         // the top eigenvalue to 1e-9 of the scale, enough for the residual
-        // estimate; to 2e-16 where the run may stop here (its Ritz pair is
-        // then the result)
+        // estimate, unless this check was predicted to end the run; to 2e-16
+        // where the run may stop here (its Ritz pair is then the result)
+        const bool full = flags[6] != 0;
         SturmBracket sb = sturm_init(alpha, beta, j + 1, lane, hint_theta, hint_r, h, ty);  // h, ty idle here
-        sturm_passes(sb, j + 1, lane, h, ty, 1e-9 * sb.scale);
+        sturm_passes(sb, j + 1, lane, h, ty, (full ? 2e-16 : 1e-9) * sb.scale);
         double theta = 0.5 * (sb.lo + sb.hi);
         NR_STAMP(13);  // Ritz check: the top eigenvalue (Sturm multisection)
         double resid = tri_top_resid(alpha, beta, j + 1, theta, beta_j, ty, lane);
-        if ((resid <= 1e3 * NR_LZ_TOL * fabs(theta) || last || !(beta_j > 1e-300 * fabs(theta))) &&
+        if (!full && (resid <= 1e3 * NR_LZ_TOL * fabs(theta) || last || !(beta_j > 1e-300 * fabs(theta))) &&
             sb.hi - sb.lo > 2e-16 * sb.scale) {
           sturm_coeffs(alpha, beta, j + 1, lane, sb.inv, h, ty);  // ty held the residual's reciprocals
           sturm_passes(sb, j + 1, lane, h, ty, 2e-16 * sb.scale);
@@ -1722,12 +1727,15 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
           }
           if (last && !conv && P.diag) atomicAdd(P.diag, 1);  // step cap hit
           int step = 8;
+          bool pred = false;
           if (prev_j > 0 && resid < prev_r && resid > 0.0) {
             const double lr = nr_log2_fast(resid);
             const double rate = (lr - nr_log2_fast(prev_r)) / (double)(j + 1 - prev_j);  // < 0
             const double need = ceil((nr_log2_fast(tol) - lr) / rate);
             step = need < 1.0 ? 1 : (need > 8.0 ? 8 : (int)need);
+            pred = need <= 8.0;
           }
+          flags[6] = pred;
           prev_j = j + 1;
           prev_r = resid;
           s_next_check = min(j + 1 + step, mcap);

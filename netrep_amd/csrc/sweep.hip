@@ -379,12 +379,13 @@ __device__ __forceinline__ void sw_block(const void* colv_, int64_t row0, const 
     const double av = fabs(y);
     A.plain += av;
     if (gj != WD_NO_GRID) {  // workgroup-uniform
-      const bool is_ff = same && e == pj + 2;
+      // every fixed-point term into `fine`, the tail's into `tn` too; the
+      // record subtracts tn and the first term after the diagonal (entry
+      // pj + 2, which sw_ff takes out of the sum: the same integers, exact)
       const bool is_tail = same && e > pj + 2;
-      A.ff += is_ff ? av : 0.0;
       const unsigned long long fx = sw_fx(ldexp(av, (is_tail ? 0 : WD_FX_BITS) - gj));
       A.tn += is_tail ? fx : 0ull;
-      A.fine += (is_tail || is_ff) ? 0ull : fx;
+      A.fine += fx;
     }
     if constexpr (X) {
       // CorrVector pair (ii = r, jj), complete cases (src/netStats.cpp:43-61)
@@ -409,6 +410,32 @@ __device__ __forceinline__ void sw_block(const void* colv_, int64_t row0, const 
     // entry's branch would be waited for with everything issued before it)
 #pragma unroll
     for (int t = 0; t < kSweepPre; ++t) asm volatile("" ::"v"(xv[t]));
+  }
+}
+
+// The first same-parity term after the diagonal (entry pj + 2 of the item's
+// sorted order, if it lies in this chunk) on the lane whose entries hold it:
+// its plain value is the record's ff part, and its fixed-point value comes out
+// of `fine` (sw_block added it there). Then `fine` drops the tail's terms,
+// which sw_block added to both. (Round 6: per pair this was a compare and two
+// selects in sw_block; C4's column sweep is issue-bound.)
+template <bool X, int L>
+__device__ __forceinline__ void sw_ff(const SwRsrc& R, const void* colv_, int64_t row0, const SwOcc& q, uint32_t bd,
+                                      int gl, int gj, SwAcc& A) {
+  using E = typename std::conditional<X, double2, double>::type;
+  const E* colv = reinterpret_cast<const E*>(colv_);
+  if (gj == WD_NO_GRID) return;  // workgroup-uniform
+  A.fine -= A.tn;
+  const int e0 = (int)(bd & 0xFFFFu), e1 = (int)(bd >> 16);
+  const int ef = (int)(q.mt.y >> 16) + 2;
+  if (ef >= e0 && ef < e1 && (ef - e0 - gl) % L == 0) {
+    const uint32_t u = __builtin_amdgcn_raw_buffer_load_b32(R.sorted, (q.mt.x + (uint32_t)ef) * 4u, 0, 0);
+    const E v = colv[(int64_t)(u >> 16) - row0];
+    double y;
+    if constexpr (X) y = v.y; else y = v;
+    const double av = fabs(y);
+    A.ff = av;
+    A.fine -= sw_fx(ldexp(av, WD_FX_BITS - gj));
   }
 }
 
@@ -504,6 +531,7 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
         sw_block<X, FIN, L>(colv, row0, cur, bdc, gl, t0, ux, xv, gj, A);
       }
     }
+    sw_ff<X, L>(R, colv, row0, cur, bdc, gl, gj, A);
     // record fields: 0 plain, 1 ff, 2..7 the CorrVector sums sx, sy, sxx, syy,
     // sxy, sum sign(x) y, 8 their pair count (not written for finite data),
     // 9..11 the fixed-point parts
