@@ -112,6 +112,8 @@ struct nr_ctx {
   size_t stage2_cap = 0;
   double* h_scale = nullptr;  // nr_scale's pinned staging (4 column chunks)
   size_t scale_cap = 0;
+  double* d_scale = nullptr;  // and its device chunks (kept between calls, released as scratch)
+  size_t d_scale_cap = 0;
   hipEvent_t ev_copy[2] = {nullptr, nullptr};
 
   // The observed statistics' own lane (nr_observed_async): stream, scratch and
@@ -1196,6 +1198,7 @@ void nr_ctx_destroy(nr_ctx* ctx) {
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_stage2) (void)hipHostFree(ctx->h_stage2);
   if (ctx->h_scale) (void)hipHostFree(ctx->h_scale);
+  dfree(ctx->d_scale);
   for (auto& ev : ctx->ev)
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : ctx->ev_copy)
@@ -1244,6 +1247,33 @@ static void parallel_copy(double* dst, const double* src, int64_t n, int threads
   for (int t = 0; t < nt; ++t) {
     const int64_t a = t * part, b = std::min(n, a + part);
     if (a < b) th.emplace_back([=]() { std::memcpy(dst + a, src + a, (size_t)(b - a) * sizeof(double)); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// Two independent copies in one fork-join, split over the threads in
+// proportion to their lengths (nr_scale: one chunk in, the previous out).
+static void parallel_copy2(double* d1, const double* s1, int64_t n1, double* d2, const double* s2, int64_t n2,
+                           int threads, int64_t min_part) {
+  const int64_t n = n1 + n2;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n / min_part));
+  if (nt == 1) {
+    if (n1) std::memcpy(d1, s1, (size_t)n1 * sizeof(double));
+    if (n2) std::memcpy(d2, s2, (size_t)n2 * sizeof(double));
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t part = (n + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t) {
+    const int64_t a = t * part, b = std::min(n, a + part);
+    if (a >= b) continue;
+    th.emplace_back([=]() {  // [a, b) of the concatenation of the two ranges
+      if (a < n1) std::memcpy(d1 + a, s1 + a, (size_t)(std::min(b, n1) - a) * sizeof(double));
+      if (b > n1) {
+        const int64_t a2 = std::max(a, n1) - n1, b2 = b - n1;
+        std::memcpy(d2 + a2, s2 + a2, (size_t)(b2 - a2) * sizeof(double));
+      }
+    });
   }
   for (auto& x : th) x.join();
 }
@@ -1781,6 +1811,8 @@ int nr_release_scratch(nr_ctx* ctx) {
   }
   dfree(ctx->d_out);
   ctx->out_cap = 0;
+  dfree(ctx->d_scale);
+  ctx->d_scale_cap = 0;
   dfree(ctx->d_out2);
   ctx->out2_cap = 0;
   dfree(ctx->d_pi);
@@ -2149,54 +2181,57 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
   return rc;
 }
 
-// Scale (src/scale.cpp:38-45) of a host matrix: column chunks of ~8 MiB
-// through the context's pinned staging buffers, double-buffered. Host threads
-// copy chunk i into pinned memory while the copy engine and the kernel work
-// on chunk i-1, then copy chunk i-1's result out of pinned memory. The
-// caller's pageable arrays are never handed to the DMA engine directly (that
-// ran at ~5 GB/s: 31 ms for 20k x 500, profiles/r05/props/).
+// Scale (src/scale.cpp:38-45) of a host matrix: column chunks of ~16 MiB
+// through the context's pinned staging buffers, double-buffered, and its
+// device chunks (both kept between calls). After chunk i is queued (copy in,
+// scale_kernel, copy out), one fork-join of the host threads copies chunk
+// i-1's result out of pinned memory and chunk i+1 into it, while the copy
+// engine and the kernel work on chunk i. The caller's pageable arrays are
+// never handed to the DMA engine directly (that ran at ~5 GB/s: 31 ms for
+// 20k x 500, profiles/r05/props/; round 6's first pinned version, one
+// fork-join per copy and a device allocation per call: 10.3 ms,
+// profiles/r06/ab5/props/).
 int nr_scale(nr_ctx* ctx, const double* data, int64_t n_samples, int64_t n_nodes, double* scaled) {
   if (!ctx || !data || !scaled || n_samples <= 0 || n_nodes <= 0) return NR_ERR_INVALID;
   NR_HIP(ctx, hipSetDevice(ctx->device));
   const int64_t S = n_samples;
-  const int64_t cols = std::max<int64_t>(1, std::min<int64_t>(n_nodes, ((int64_t)1 << 20) / S));
+  const int64_t cols = std::max<int64_t>(1, std::min<int64_t>(n_nodes, ((int64_t)1 << 21) / S));
   const int64_t chunk = cols * S;  // doubles per chunk
   if (int rc = ensure_stage(ctx, ctx->h_scale, ctx->scale_cap, (size_t)(4 * chunk))) return rc;
+  if (int rc = ensure(ctx, ctx->d_scale, ctx->d_scale_cap, (size_t)(4 * chunk))) return rc;
   double* hin[2] = {ctx->h_scale, ctx->h_scale + chunk};
   double* hout[2] = {ctx->h_scale + 2 * chunk, ctx->h_scale + 3 * chunk};
-  double* dbuf = nullptr;
-  NR_HIP(ctx, hipMalloc((void**)&dbuf, (size_t)(4 * chunk) * sizeof(double)));
-  double* din[2] = {dbuf, dbuf + chunk};
-  double* dout[2] = {dbuf + 2 * chunk, dbuf + 3 * chunk};
+  double* din[2] = {ctx->d_scale, ctx->d_scale + chunk};
+  double* dout[2] = {ctx->d_scale + 2 * chunk, ctx->d_scale + 3 * chunk};
   hipEvent_t ev[2] = {nullptr, nullptr};
   hipError_t e = hipSuccess;
   for (int b = 0; b < 2 && e == hipSuccess; ++b) e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
   const int threads = ctx->host_threads;
   const int64_t n_chunks = (n_nodes + cols - 1) / cols;
-  auto drain = [&](int64_t i) {  // chunk i's result from pinned memory to the caller
-    const int b = (int)(i & 1);
-    const int64_t c0 = i * cols, nc = std::min(cols, n_nodes - c0);
-    e = hipEventSynchronize(ev[b]);
-    if (e == hipSuccess) parallel_copy(scaled + c0 * S, hout[b], nc * S, threads, (int64_t)1 << 17);
-  };
+  auto len = [&](int64_t i) { return std::min(cols, n_nodes - i * cols) * S; };
+  if (e == hipSuccess) parallel_copy(hin[0], data, len(0), threads, (int64_t)1 << 17);
   for (int64_t i = 0; i < n_chunks && e == hipSuccess; ++i) {
     const int b = (int)(i & 1);
-    const int64_t c0 = i * cols, nc = std::min(cols, n_nodes - c0);
-    // hin[b] / hout[b] were last used by chunk i-2, drained (event waited) in iteration i-1
-    parallel_copy(hin[b], data + c0 * S, nc * S, threads, (int64_t)1 << 17);
-    e = h2d_async(din[b], hin[b], (size_t)(nc * S) * sizeof(double), ctx->stream);
-    if (e == hipSuccess) e = nr::launch_scale(din[b], dout[b], S, nc, ctx->stream);
+    // hin[b] holds chunk i; hout[b] was drained in iteration i-1 (chunk i-2)
+    e = h2d_async(din[b], hin[b], (size_t)len(i) * sizeof(double), ctx->stream);
+    if (e == hipSuccess) e = nr::launch_scale(din[b], dout[b], S, len(i) / S, ctx->stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(hout[b], dout[b], (size_t)(nc * S) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+      e = hipMemcpyAsync(hout[b], dout[b], (size_t)len(i) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ev[b], ctx->stream);
-    if (e == hipSuccess && i >= 1) drain(i - 1);
+    // chunk i-1 done (its pinned input free for chunk i+1, its result ready)
+    if (e == hipSuccess && i >= 1) e = hipEventSynchronize(ev[b ^ 1]);
+    if (e != hipSuccess) break;
+    const bool out = i >= 1, in = i + 1 < n_chunks;
+    parallel_copy2(out ? scaled + (i - 1) * cols * S : scaled, hout[b ^ 1], out ? len(i - 1) : 0, hin[b ^ 1],
+                   in ? data + (i + 1) * cols * S : data, in ? len(i + 1) : 0, threads, (int64_t)1 << 17);
   }
-  if (e == hipSuccess) drain(n_chunks - 1);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipEventSynchronize(ev[(n_chunks - 1) & 1]);
+  if (e == hipSuccess)
+    parallel_copy(scaled + (n_chunks - 1) * cols * S, hout[(n_chunks - 1) & 1], len(n_chunks - 1), threads,
+                  (int64_t)1 << 17);
   (void)hipStreamSynchronize(ctx->stream);
   for (hipEvent_t x : ev)
     if (x) (void)hipEventDestroy(x);
-  (void)hipFree(dbuf);
   if (e != hipSuccess) return hip_fail(ctx, e, "scale");
   return NR_OK;
 }

@@ -56,11 +56,12 @@ def test_scale_matches_oracle(bundled, bundled_expected):
     assert_stats_close(got, bundled_expected["scaled_test_data"], rtol=1e-13, floor=1.0, what="Scale")
 
 
-@pytest.mark.parametrize("s,n", [(37, 100_003), (1_100_000, 3), (500, 1)])
+@pytest.mark.parametrize("s,n", [(37, 100_003), (500, 20_000), (1_100_000, 3), (500, 1)])
 def test_scale_column_chunks_match_oracle(s, n):
-    """netrep_Scale streams ~8 MiB column chunks through pinned staging: many
-    chunks with a ragged last one, one column longer than a chunk, a single
-    column. Every column as src/scale.cpp:14-25 (numpy restatement), with a
+    """netrep_Scale streams ~16 MiB column chunks through pinned staging, each
+    fork-join of the host threads copying one chunk in and the previous one
+    out: two chunks with a ragged last one, five (the metric's 20k x 500), one
+    column longer than a chunk, a single column. Every column as src/scale.cpp:14-25 (numpy restatement), with a
     constant column (sd 0: NaN, as the reference gives)."""
     from oracle import netrep_oracle as O
     rng = np.random.default_rng(s + n)
