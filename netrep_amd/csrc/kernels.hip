@@ -1772,8 +1772,18 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     }
   } else {
     for (int c = tid; c < k; c += BS) {
+      // eight basis entries' loads in flight at a time (the same sum, in the
+      // same order: one dependent global load per step otherwise)
       double s = 0.0;
-      for (int i = 0; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
+      int i = 0;
+      for (; i + 8 <= nsteps; i += 8) {
+        double q8[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) q8[t] = Q[(int64_t)(i + t) * k + c];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s += ty[i + t] * q8[t];
+      }
+      for (; i < nsteps; ++i) s += ty[i] * Q[(int64_t)i * k + c];
       L.vv[c] = s;
       if (gv_out) L.gv[c] = theta_f * s + ym * w[c];
       nv[0] += s * s;

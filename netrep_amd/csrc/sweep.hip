@@ -520,26 +520,15 @@ __global__ void __launch_bounds__(kSweepWaves * 64) sweep_column_kernel(SweepPar
     sw_entries<L>(R, nxt, sw_range(P, nxt, h), gl, 0, un);
     SwOcc nn;
     sw_fetch<X>(P, R, h, sb + 2 * stride + grp, o1, nn);
-    // the current occurrences' second block of entries, in flight during the
-    // first block's sums (read whether or not the ranges reach it: in-range
-    // offsets, never used past the range); each later block's entries load
-    // while the block before is summed. (Round 6: at C4's ~13 entries per lane
-    // and chunk, the second block's entries and then its discovery values were
-    // two dependent global-load latencies on every batch, with the column
-    // kernel waiting on loads, not issue-bound: profiles/r06/ab5/.)
-    uint32_t ux[kSweepPre];
-    sw_entries<L>(R, cur, bdc, gl, kSweepPre, ux);
     SwAcc A;
     sw_block<X, FIN, L>(colv, row0, cur, bdc, gl, 0, uc, xv, gj, A);
     {
       const int e0 = (int)(bdc & 0xFFFFu), e1 = (int)(bdc >> 16);
       for (int t0 = kSweepPre; e0 + L * t0 < e1; t0 += kSweepPre) {  // long chunk ranges
+        uint32_t ux[kSweepPre];
+        sw_entries<L>(R, cur, bdc, gl, t0, ux);
         if (X) sw_xv(R, cur, ux, xv);
-        uint32_t uy[kSweepPre];
-        sw_entries<L>(R, cur, bdc, gl, t0 + kSweepPre, uy);
         sw_block<X, FIN, L>(colv, row0, cur, bdc, gl, t0, ux, xv, gj, A);
-#pragma unroll
-        for (int t = 0; t < kSweepPre; ++t) ux[t] = uy[t];
       }
     }
     sw_ff<X, L>(R, colv, row0, cur, bdc, gl, gj, A);
