@@ -84,21 +84,22 @@ def test_bench_traffic_lookup_matches_committed_pmc():
     config, batch and kernel (profiles/pmc_traffic.json), as a [raw, x2] range
     with the pass's kernel time next to this run's (traffic_time_ratio)."""
     import bench
-    t = bench.traffic_fields("C3", 5120, "module_profile_kernel", 260.0, table=True)
+    t = bench.traffic_fields("C3", 5120, "module_profile_kernel", 254.0, table=True)
     assert t["traffic"] is not None and t["traffic"] > 0
     raw, x2 = t["traffic_range"]
     assert 0 < raw <= x2 == t["traffic"]
-    assert abs(t["traffic_time_ratio"] - 1.0) < 0.01     # the r05 final-tree pass: 260.42 ms
+    assert abs(t["traffic_time_ratio"] - 1.0) < 0.01     # the r06 final-tree pass: 253.79 ms
     # superseded rows (passes of kernels since replaced) are never reported
     assert bench.traffic_fields("C3", 256, "module_profile_kernel", 17.9)["traffic"] is None
     assert bench.traffic_fields("C3", 512, "module_profile_kernel", 1.0)["traffic"] is None
     assert bench.traffic_fields("C2", 256, "module_profile_kernel", 1.0)["traffic"] is None
-    # a launch within 10% of a pass's size (the reference interface's own
-    # launches, 66 permutations at C5): the pass scaled by the size, marked
-    t66 = bench.traffic_fields("C5", 66, "module_profile_kernel", 50.0)   # the three-dataset pass
-    t70 = bench.traffic_fields("C5", 70, "module_profile_kernel", 50.0)
-    assert "traffic_scaled_from_batch" not in t66 and t70["traffic_scaled_from_batch"] == 66
-    assert abs(t70["traffic"] / t66["traffic"] - 70 / 66) < 1e-12
+    # a launch within 10% of a pass's size (the reference interface sizes
+    # its own launches, e.g. 66 permutations at C5): the pass scaled by the
+    # size, marked
+    t64 = bench.traffic_fields("C5", 64, "module_profile_kernel", 50.0)   # the three-dataset pass
+    t66 = bench.traffic_fields("C5", 66, "module_profile_kernel", 50.0)
+    assert "traffic_scaled_from_batch" not in t64 and t66["traffic_scaled_from_batch"] == 64
+    assert abs(t66["traffic"] / t64["traffic"] - 66 / 64) < 1e-12
     assert bench.traffic_fields("C5", 80, "module_profile_kernel", 50.0)["traffic"] is None  # > 10% off
 
 
