@@ -256,7 +256,10 @@ int nr_synchronize(nr_ctx* ctx);
  * summed over workgroups, 16 slots (0 index, 1 Gram, 2 Lanczos set-up,
  * 3 matvec, 4 three-term step + omega, 5 statistics, 6 q update, 7 Ritz
  * checks, 8 start column, 9 reorthogonalisation, 10 Ritz vector,
- * 11 node contributions, 12 Ritz coefficients; 13-15 spare). Off by default; a run with stamps on
+ * 11 node contributions, 12 Ritz coefficients, 13 a Ritz check's top
+ * eigenvalue, 14 its residual (and the full-precision refinement where the
+ * check may end the run; 7 keeps the rest of the check); 15 spare). Off by
+ * default; a diagnostic build (make EXTRA=-DNR_STAMPS=1) records them; a run with stamps on
  * is a measurement run, not a timed one. */
 int nr_set_stamps(nr_ctx* ctx, int enable);
 int nr_get_stamps(nr_ctx* ctx, uint64_t* cycles);
@@ -420,7 +423,8 @@ int netrep_NetProps(const double* data, const double* net, int64_t n_samples,
                     double* coherence_out, double* avg_weight_out,
                     int64_t* k_all_out);
 
-/* Scale (src/scale.cpp:38-45). */
+/* Scale (src/scale.cpp:38-45): the host matrix through the context's pinned
+ * staging in ~16 MiB column chunks, scaled on the device, copied back. */
 int netrep_Scale(const double* data, int64_t n_samples, int64_t n_nodes,
                  double* scaled_out);
 
