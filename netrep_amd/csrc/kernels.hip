@@ -1122,6 +1122,165 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
   }
 }
 
+// The large modules' Gram in 64 x 128 super-tiles per wave (round 6): a
+// 64-wide column panel (4 blocks of 16) against a 128-wide row panel (8
+// blocks), 4 x 8 MFMA tiles held in the wave's 256 accumulator registers.
+// Twelve operand blocks per 16-deep step feed 32 tiles (gram_mfma64: eight
+// feed 16), a quarter fewer operand reads per MFMA from L2 / the Infinity
+// Cache, where the 64 x 64 scheme's Gram phase waits (38% MFMA-busy,
+// profiles/r05/c5gram/). Tiles above the diagonal (row block < column block)
+// are skipped; the same operand layout, K order, packed stores and epilogue
+// as gram_mfma64 otherwise.
+template <int NW, bool DUAL, int RW = 8>
+__device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t* idx, int k, int64_t ones_off,
+                             double* __restrict__ G, float* __restrict__ G32, double& g1sum, int& bad) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int kc = DUAL ? S + 1 : k + 1;
+  const int RB = (kc + 15) / 16;  // 16-blocks of the side
+  const int T4 = (RB + 3) / 4, T8 = (RB + RW - 1) / RW;
+  int nsup = 0;
+  for (int I4 = 0; I4 < T4; ++I4) nsup += T8 - 4 * I4 / RW;
+  const int full = S / 16 * 16;
+  for (int t = wave; t < nsup; t += NW) {
+    int I4 = 0, rem = t;
+    while (rem >= T8 - 4 * I4 / RW) {
+      rem -= T8 - 4 * I4 / RW;
+      ++I4;
+    }
+    const int R8 = 4 * I4 / RW + rem;
+    // row block 8 R8 + b >= column block 4 I4 + a, i.e. b >= a + d (uniform per super-tile)
+    const int d = 4 * I4 - RW * R8;  // -4 * (odd/even offset) .. 4
+    // operand blocks: o < 4 the column side (16 (4 I4 + o) + i16), o >= 4 the row side (16 (8 R8 + o - 4) + i16)
+    const double* col[4 + RW];
+    int cs[4 + RW];
+#pragma unroll
+    for (int o = 0; o < 4 + RW; ++o) {
+      const int c = (o < 4 ? 4 * I4 + o : RW * R8 + o - 4) * 16 + i16;
+      cs[o] = c;
+      if (!DUAL) {
+        const int64_t off = c < k ? (int64_t)idx[c] * S : (c == k ? ones_off : ones_off + S);
+        col[o] = X + off + 4 * kk;
+      }
+    }
+    nr_f64x4 acc[4][RW];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < RW; ++b) acc[a][b] = nr_f64x4{0.0, 0.0, 0.0, 0.0};
+    // one register set of operands, refilled column q by column q: once a
+    // step's MFMAs have read v[.][q], the next step's v[.][q] is loaded into
+    // the same registers while the MFMAs of q + 1.. run (96 VGPRs of operands
+    // instead of two 96-register sets; the loads are unconditional -- the
+    // last step re-reads its own operands -- so the waits count them exactly)
+    double v[4 + RW][4];
+    // every tile of the super-tile, the ones above the diagonal too (not
+    // stored): a branch per tile split the loop and spilled; the extra MFMAs
+    // (~10% over the triangle) are free in this operand-bound phase
+    auto mfma_q = [&](int q) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < RW; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[a][q], v[4 + b][q], acc[a][b], 0, 0, 0);
+    };
+    if (!DUAL) {
+      auto ldp = [&](int s0, int qp) {  // samples s0 + 4 kk + 2 qp, + 1 of every operand column
+#pragma unroll
+        for (int o = 0; o < 4 + RW; ++o) {
+          double2 p;
+          __builtin_memcpy(&p, col[o] + s0 + 2 * qp, sizeof(double2));
+          v[o][2 * qp] = p.x;
+          v[o][2 * qp + 1] = p.y;
+        }
+      };
+      if (full > 0) {
+        ldp(0, 0);
+        ldp(0, 1);
+      }
+      for (int s0 = 0; s0 < full; s0 += 16) {
+        const int sn = s0 + 16 < full ? s0 + 16 : s0;
+        mfma_q(0);
+        mfma_q(1);
+        ldp(sn, 0);
+        mfma_q(2);
+        mfma_q(3);
+        ldp(sn, 1);
+      }
+      if (full < S) {  // the last, partial step
+#pragma unroll
+        for (int o = 0; o < 4 + RW; ++o)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[o][q] = full + 4 * kk + q < S ? col[o][full + q] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mfma_q(q);
+      }
+    } else {
+      // operand columns are samples (S: the ones row, beyond: zero), the
+      // contraction over the k nodes, 16 per step (node c0 + 4 kk + q in
+      // column q); super-tiles whose row panel lies inside the first S
+      // samples load at immediate offsets
+      const bool interior = 16 * RW * R8 + 16 * RW <= S;
+      auto ldq = [&](int c, int q) {
+        const bool valid = c < k;
+        const double* colp = X + (int64_t)idx[valid ? c : k - 1] * S;
+        if (interior) {
+          const double* pi = colp + 64 * I4 + i16;
+          const double* pj = colp + 16 * RW * R8 + i16;
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            const double xi = pi[16 * o];
+            v[o][q] = valid ? xi : 0.0;
+          }
+#pragma unroll
+          for (int o = 0; o < RW; ++o) {
+            const double xj = pj[16 * o];
+            v[4 + o][q] = valid ? xj : 0.0;
+          }
+        } else {
+#pragma unroll
+          for (int o = 0; o < 4 + RW; ++o) {
+            const double x = cs[o] < S ? colp[cs[o]] : (cs[o] == S ? 1.0 : 0.0);
+            v[o][q] = valid ? x : 0.0;
+          }
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ldq(4 * kk + q, q);
+      for (int c0 = 0; c0 < k; c0 += 16) {
+        const int cn = c0 + 16 < k ? c0 + 16 : c0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          mfma_q(q);
+          ldq(cn + 4 * kk + q, q);
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < RW; ++b) {
+        if (b < a + d) continue;
+        const int gc = 4 * I4 + a, gr = RW * R8 + b;
+        pk_store_tile16(G, G32, kc, gc, gr, acc[a][b], lane);
+        const double wgt = gc == gr ? 1.0 : 2.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = gc * 16 + kk + 4 * r;
+          const int gj = gr * 16 + i16;
+          const double val = acc[a][b][r];
+          if (DUAL) {
+            if (gj == S && gi < S) g1sum += val * val;
+            if (gi == gj && gi < S) bad |= (int)!isfinite(val);
+          } else {
+            if (gi < k && gj < k) g1sum += wgt * val;
+            if (gi == gj && gi < k) bad |= (int)!isfinite(val);
+          }
+        }
+      }
+  }
+}
+
 // Dual Gram for modules with more nodes than samples (k > S): H = [X' 1]' [X' 1]
 // over the k module nodes, i.e. X X' (S x S) bordered by the row sums X 1 and
 // k. Its top eigenvector is the summary profile u itself (the left singular
@@ -1916,7 +2075,11 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     if (G64) {
       if (dual)
+#ifdef NR_G128
+        gram_mfma128<NW, true, NR_G128>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
+#else
         gram_mfma64<NW, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
+#endif
       else
         gram_mfma64<NW, false>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad);
     } else if (!TABLE) {
