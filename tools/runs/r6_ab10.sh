@@ -1,0 +1,23 @@
+# Round 6 A/B 10 on C2: the wave class's Gram with one register set of
+# operands refilled column by column (wave) against the in-tree two-set
+# version (ritz), alternating; then wave in place of the in-tree library for
+# the wave-class parity tests.
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+D=gpurun_out/r6ab10
+mkdir -p $D
+( while sleep 50; do date >> $D/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+A=netrep_amd/_lib/ab
+B="python -u bench.py --no-secondary --no-cpu-baseline --steps 10 --config C2"
+for i in 1 2; do
+  for v in ritz wave; do
+    timeout -k 10 300 $B --lib $A/lib$v.so > $D/${v}_C2.$i.json 2> $D/${v}_C2.$i.err
+  done
+done
+cp $A/libwave.so netrep_amd/_lib/libnetrep_amd.so
+rm -f gpurun_out/parity_maxerr.json
+timeout -k 10 700 python -u -m pytest tests/test_gpu_small.py tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -x -v -k "c2 or small or wave or bundled or golden or driver" --timeout 500 --timeout-method thread > $D/pytest.txt 2>&1
+cp gpurun_out/parity_maxerr.json $D/
