@@ -1122,16 +1122,23 @@ __device__ void gram_mfma64(const double* __restrict__ X, int S, const uint32_t*
   }
 }
 
-// The large modules' Gram in 64 x 128 super-tiles per wave (round 6): a
-// 64-wide column panel (4 blocks of 16) against a 128-wide row panel (8
-// blocks), 4 x 8 MFMA tiles held in the wave's 256 accumulator registers.
-// Twelve operand blocks per 16-deep step feed 32 tiles (gram_mfma64: eight
-// feed 16), a quarter fewer operand reads per MFMA from L2 / the Infinity
-// Cache, where the 64 x 64 scheme's Gram phase waits (38% MFMA-busy,
-// profiles/r05/c5gram/). Tiles above the diagonal (row block < column block)
-// are skipped; the same operand layout, K order, packed stores and epilogue
-// as gram_mfma64 otherwise.
-template <int NW, bool DUAL, int RW = 8>
+// The large modules' dual Gram in 64 x 16 RW super-tiles per wave (round 6):
+// a 64-wide column panel (4 blocks of 16) against a 16 RW-wide row panel (RW
+// blocks), 4 x RW MFMA tiles in the wave's accumulator registers, with one
+// register set of operands refilled column by column. 4 + RW operand blocks
+// per 16-deep step feed 4 RW tiles (gram_mfma64: 8 feed 16), fewer operand
+// reads per MFMA from L2 / the Infinity Cache, where the 64 x 64 scheme's
+// Gram phase waits (38% MFMA-busy, profiles/r05/c5gram/). Every tile is
+// computed, those above the diagonal (row block < column block) are not
+// stored; the same operand layout, K order (bitwise the same Gram), packed
+// stores and epilogue as gram_mfma64 otherwise. Measured on C5 (10,000
+// permutations per dataset, profiles/r06/ab_gram/): RW = 4 (the rolling
+// buffer alone) 984 perms/s, 6: 1,007, 7: 1,031, against 967 for
+// gram_mfma64; RW = 8 (all 256 accumulator registers) spills ~1.1 KB per
+// lane. The primal Gram (k <= S) keeps gram_mfma64: its 64 x 80 version was
+// slower (997) and its 64 x 64 rolling version equal (1,007).
+constexpr int kGramDualRows = 7;
+template <int NW, bool DUAL, int RW>
 __device__ void gram_mfma128(const double* __restrict__ X, int S, const uint32_t* idx, int k, int64_t ones_off,
                              double* __restrict__ G, float* __restrict__ G32, double& g1sum, int& bad) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2075,17 +2082,9 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
     // ---- Gram [X 1]^T [X 1] on the matrix cores (S x S dual when k > S) ----
     if (G64) {
       if (dual)
-#ifdef NR_G128
-        gram_mfma128<NW, true, NR_G128>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
-#else
-        gram_mfma64<NW, true>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
-#endif
+        gram_mfma128<NW, true, kGramDualRows>(X, S, Li.idx, k, P.ones_off, G, G32, g1[0], bad);
       else
-#ifdef NR_G128P
-        gram_mfma128<NW, false, NR_G128P>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad);
-#else
         gram_mfma64<NW, false>(X, S, L.idx, k, P.ones_off, G, G32, g1[0], bad);
-#endif
     } else if (!TABLE) {
       if (dual)
         gram_mfma_dual<NW, PACKED>(X, S, Li.idx, k, G, G32, ld, g1[0], bad);
