@@ -2228,50 +2228,50 @@ __device__ __forceinline__ void gram_wave(const double* __restrict__ X, int S, c
     const int c = 16 * I + i16;
     col[I] = c < k ? (int)idx[c] * S : (int)(c == k ? ones_off : ones_off + S);
   }
-  // column q of step st's operands into v[.][q]
-  auto ldq = [&](int st, int q, double (&v)[kWaveBlocks][4]) {
+  auto ld = [&](int st, double (&v)[kWaveBlocks][4]) {
     if (!dual) {
       const int s0 = 16 * st + 4 * kk;
 #pragma unroll
-      for (int I = 0; I < kWaveBlocks; ++I) {
-        const int vo = I < nb && s0 + q < S ? (col[I] + s0 + q) * 8 : OOR;
-        v[I][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, 0, 0));
-      }
-    } else {
-      const int c = 16 * st + 4 * kk + q;
-      const int base = c < k ? (int)idx[c] * S : 0;
+      for (int I = 0; I < kWaveBlocks; ++I)
 #pragma unroll
-      for (int I = 0; I < kWaveBlocks; ++I) {
-        const int s = 16 * I + i16;
-        const int vo = I < nb && c < k && s < S ? (base + s) * 8 : OOR;
-        const double x = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, 0, 0));
-        v[I][q] = s == S && c < k ? 1.0 : x;  // the ones row
+        for (int q = 0; q < 4; ++q) {
+          const int vo = I < nb && s0 + q < S ? (col[I] + s0 + q) * 8 : OOR;
+          v[I][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, 0, 0));
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 16 * st + 4 * kk + q;
+        const int base = c < k ? (int)idx[c] * S : 0;
+#pragma unroll
+        for (int I = 0; I < kWaveBlocks; ++I) {
+          const int s = 16 * I + i16;
+          const int vo = I < nb && c < k && s < S ? (base + s) * 8 : OOR;
+          const double x = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo, 0, 0));
+          v[I][q] = s == S && c < k ? 1.0 : x;  // the ones row
+        }
       }
     }
   };
-  // One register set of operands, refilled column by column (round 6, as
-  // gram_mfma128): once a step's MFMAs have read v[.][q], the next step's
-  // v[.][q] loads into the same registers while the MFMAs of q + 1.. run (28
-  // doubles of operands instead of two sets of 28). The last step re-reads
-  // its own operands (unconditional loads: the waits count them exactly).
   const int nsteps = dual ? (k + 15) / 16 : (S + 15) / 16;
-  double v[kWaveBlocks][4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) ldq(0, q, v);
+  double cur[kWaveBlocks][4], nxt[kWaveBlocks][4];
+  ld(0, cur);
   for (int st = 0; st < nsteps; ++st) {
-    const int sn = st + 1 < nsteps ? st + 1 : st;
+    if (st + 1 < nsteps) ld(st + 1, nxt);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int I = 0; I < kWaveBlocks; ++I) {
         if (I >= nb) break;
 #pragma unroll
         for (int J = 0; J <= I; ++J)
           T[wave_tile(I, J)] =
-              __builtin_amdgcn_mfma_f64_16x16x4f64(v[I][q], v[J][q], T[wave_tile(I, J)], 0, 0, 0);
+              __builtin_amdgcn_mfma_f64_16x16x4f64(cur[I][q], cur[J][q], T[wave_tile(I, J)], 0, 0, 0);
       }
-      ldq(sn, q, v);
-    }
+#pragma unroll
+    for (int I = 0; I < kWaveBlocks; ++I)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[I][q] = nxt[I][q];
   }
 }
 
