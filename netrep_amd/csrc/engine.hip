@@ -2182,8 +2182,9 @@ int nr_module_vectors(nr_ctx* ctx, int32_t n_mod, const int64_t* node_off, const
 }
 
 // Scale (src/scale.cpp:38-45) of a host matrix: column chunks of ~16 MiB
-// through the context's pinned staging buffers, double-buffered, and its
-// device chunks (both kept between calls). After chunk i is queued (copy in,
+// through the context's pinned staging buffers (kept between calls),
+// double-buffered, and its device chunks (scratch: nr_release_scratch frees
+// them, as a pooled context's return does). After chunk i is queued (copy in,
 // scale_kernel, copy out), one fork-join of the host threads copies chunk
 // i-1's result out of pinned memory and chunk i+1 into it, while the copy
 // engine and the kernel work on chunk i. The caller's pageable arrays are
