@@ -1901,13 +1901,14 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
             step = need < 1.0 ? 1 : (need > 8.0 ? 8 : (int)need);
             pred = need <= 8.0;
           }
-#ifdef NR_CROSS_CHECK
           // Still on fp64 matvecs: also check where the decay predicts the
           // residual's crossing of the fp32 threshold (the decay since the
           // previous check, or since step 0 at residual theta for the first),
           // so the relaxed phase starts near the crossing instead of at the
           // next convergence check (offline, tools/sim_lanczos_tiers.py: Gram
-          // bytes per entry 226.8 -> 216.6, +0.25 checks)
+          // bytes per entry 226.8 -> 216.6, +0.25 checks). Neutral at round
+          // 5's check cost (profiles/r06/ab_tiers/), C3 -1.0% with the
+          // cheaper checks (profiles/r06/ab_cross/).
           if (relax && flags[5] == 0 && resid > 1e-7 * fabs(theta) && resid < fabs(theta)) {
             const double lr = nr_log2_fast(resid);
             const double rate = prev_j > 0 && resid < prev_r && resid > 0.0
@@ -1919,7 +1920,6 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
               pred = false;  // not the predicted convergence: the coarse stage suffices
             }
           }
-#endif
           flags[6] = pred;
           prev_j = j + 1;
           prev_r = resid;
