@@ -1,6 +1,6 @@
 # Round 6 final tree, part 2: the C3 and C5 PMC passes (the table kernel and
-# the large-module kernel changed), the extended parity sweep (C3 1,024, C2
-# 2,048, C5 64 permutations).
+# the large-module kernel changed), then the C5 large-item Gram alone under
+# counters (tools/runs/r6_c5gram.sh).
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -17,5 +17,5 @@ for c in C3 C5; do
   find $D/$c -name '*.csv' ! -name 'kernel_stats.csv' -delete
   find $D/$c -name '*.db' -delete
 done
-timeout -k 10 900 python -u tools/parity_sweep.py 1024 2048 64 > $D/parity_sweep.json 2> $D/parity_sweep.err
+timeout -k 10 900 bash tools/runs/r6_c5gram.sh
 du -sh gpurun_out
