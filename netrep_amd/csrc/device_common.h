@@ -278,12 +278,18 @@ static __device__ __forceinline__ double tri_top_resid(const double* alpha, cons
     ss = fma(y0, y0, ss);
     y2 = y1;
     y1 = y0;
-    if (ss > 1e200) {
-      y1 *= 1e-100;
-      y2 *= 1e-100;
-      ss *= 1e-200;
-      beta_j *= 1e-100;
-    }
+  };
+  // Overflow guard, every fourth step, by selects: the scale is a power of
+  // two (exact), so the result is the unscaled one bit for bit. Round 6: a
+  // test per step compiled to an exec-mask branch on the recurrence's chain
+  // (compare, s_and_saveexec, s_or) and tripled each step's latency. After a
+  // guard ss <= 2^256, so four steps may grow y by 2^384 before ss overflows.
+  auto renorm = [&]() {
+    const int e = ss > 0x1p256 ? -256 : 0;  // v_ldexp: no 64-bit constants to keep live
+    y1 = ldexp(y1, e);
+    y2 = ldexp(y2, e);
+    beta_j = ldexp(beta_j, e);
+    ss = ldexp(ss, 2 * e);
   };
   int i = n - 1;
   for (; i >= 8; i -= 8) {  // steps i .. i - 7, all >= 1
@@ -295,9 +301,15 @@ static __device__ __forceinline__ double tri_top_resid(const double* alpha, cons
       rv[t] = rb[i - t - 1];
     }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) step(av[t], bv[t], rv[t]);
+    for (int t = 0; t < 8; ++t) {
+      step(av[t], bv[t], rv[t]);
+      if ((t & 3) == 3) renorm();
+    }
   }
-  for (; i > 0; --i) step(alpha[i], i < n - 1 ? beta[i] : 0.0, rb[i - 1]);
+  for (; i > 0; --i) {
+    step(alpha[i], i < n - 1 ? beta[i] : 0.0, rb[i - 1]);
+    if ((i & 3) == 0) renorm();  // i is wave-uniform: a scalar branch
+  }
   return beta_j / sqrt(ss);
 }
 
