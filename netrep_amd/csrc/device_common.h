@@ -332,81 +332,204 @@ static __device__ __forceinline__ double nr_log2_fast(double x) {
 // loop behind, 12% of a C2 item). The second step starts from the first
 // step's result scaled by 1/max (proportional to the normalised vector the
 // old loop passed on: the same direction to rounding).
+// Round 6: every loop reads its operands a group of G steps ahead of the
+// recurrence (the compiler had put one LDS read and its wait on each step's
+// chain); the same arithmetic in the same order. G = 1 keeps the previous
+// loops (the large-module kernel: with the groups its register allocation
+// moved spill code into its Gram loop).
+template <int G>
 static __device__ __forceinline__ void tri_eigenvector(const double* __restrict__ alpha,
                                                        const double* __restrict__ beta, int n, double theta,
                                                        double* __restrict__ y, double* __restrict__ work) {
-  double* __restrict__ dl = work;
-  double* __restrict__ rd = work + n;   // 1 / pivot
-  double* __restrict__ du = work + 2 * n;
-  double* __restrict__ du2 = work + 3 * n;
-  double* __restrict__ swp = work + 4 * n;
-  double scale = fabs(theta);
-#pragma unroll 4
-  for (int i = 0; i < n; ++i) {
-    scale = fmax(scale, fabs(alpha[i]));
-    if (i < n - 1) scale = fmax(scale, fabs(beta[i]));
-  }
-  const double floor_piv = 1e-300 + 2.2e-16 * scale;
-  double di = alpha[0] - theta;          // current pivot candidate d_i
-  double dui = n > 1 ? beta[0] : 0.0;    // current super-diagonal du_i
-  // branch-free steps (selects instead of the two pivoting paths), so the
-  // loop unrolls and the next steps' LDS reads overlap this step's chain
-#pragma unroll 4
-  for (int i = 0; i < n - 1; ++i) {
-    const double bi = beta[i];                       // sub-diagonal dl_i
-    const double dn = alpha[i + 1] - theta;          // d_{i+1} before this step
-    const double dun = i < n - 2 ? beta[i + 1] : 0.0;  // du_{i+1} before this step
-    const bool sw = !(fabs(di) >= fabs(bi));         // row interchange
-    const double dc = fabs(di) < floor_piv ? (di < 0.0 ? -floor_piv : floor_piv) : di;
-    const double r = 1.0 / (sw ? bi : dc);
-    const double f = (sw ? di : bi) * r;
-    dl[i] = f;
-    rd[i] = r;
-    du[i] = sw ? dn : dui;
-    du2[i] = sw ? dun : 0.0;
-    swp[i] = sw ? 1.0 : 0.0;
-    const double ndi = sw ? dui - f * dn : dn - f * dui;
-    dui = sw ? -f * dun : dun;
-    di = ndi;
-  }
-  if (fabs(di) < floor_piv) di = di < 0.0 ? -floor_piv : floor_piv;
-  rd[n - 1] = 1.0 / di;
-  double sc = 1.0;  // scale of the right-hand side (1 / max of the previous iterate)
-  for (int iter = 0; iter < 2; ++iter) {
-    // L solve (the row interchanges applied as the factorisation made them)
-    double yi = iter == 0 ? 1.0 : y[0] * sc;
-#pragma unroll 4
+  if constexpr (G == 1) {  // the previous loops
+    double* __restrict__ dl = work;
+    double* __restrict__ rd = work + n;   // 1 / pivot
+    double* __restrict__ du = work + 2 * n;
+    double* __restrict__ du2 = work + 3 * n;
+    double* __restrict__ swp = work + 4 * n;
+    double scale = fabs(theta);
+  #pragma unroll 4
+    for (int i = 0; i < n; ++i) {
+      scale = fmax(scale, fabs(alpha[i]));
+      if (i < n - 1) scale = fmax(scale, fabs(beta[i]));
+    }
+    const double floor_piv = 1e-300 + 2.2e-16 * scale;
+    double di = alpha[0] - theta;          // current pivot candidate d_i
+    double dui = n > 1 ? beta[0] : 0.0;    // current super-diagonal du_i
+    // branch-free steps (selects instead of the two pivoting paths), so the
+    // loop unrolls and the next steps' LDS reads overlap this step's chain
+  #pragma unroll 4
     for (int i = 0; i < n - 1; ++i) {
-      const double yn = iter == 0 ? 1.0 : y[i + 1] * sc;
-      const bool sw = swp[i] != 0.0;
-      const double a = sw ? yn : yi, b = sw ? yi : yn;
-      y[i] = a;
-      yi = b - dl[i] * a;
+      const double bi = beta[i];                       // sub-diagonal dl_i
+      const double dn = alpha[i + 1] - theta;          // d_{i+1} before this step
+      const double dun = i < n - 2 ? beta[i + 1] : 0.0;  // du_{i+1} before this step
+      const bool sw = !(fabs(di) >= fabs(bi));         // row interchange
+      const double dc = fabs(di) < floor_piv ? (di < 0.0 ? -floor_piv : floor_piv) : di;
+      const double r = 1.0 / (sw ? bi : dc);
+      const double f = (sw ? di : bi) * r;
+      dl[i] = f;
+      rd[i] = r;
+      du[i] = sw ? dn : dui;
+      du2[i] = sw ? dun : 0.0;
+      swp[i] = sw ? 1.0 : 0.0;
+      const double ndi = sw ? dui - f * dn : dn - f * dui;
+      dui = sw ? -f * dun : dun;
+      di = ndi;
     }
-    // U solve (bandwidth 3)
-    double y1 = yi * rd[n - 1], y2 = 0.0;
-    y[n - 1] = y1;
-    double mx = fabs(y1);
-#pragma unroll 4
-    for (int i = n - 2; i >= 0; --i) {
-      const double y0 = (y[i] - du[i] * y1 - du2[i] * y2) * rd[i];
-      y[i] = y0;
-      mx = fmax(mx, fabs(y0));
-      y2 = y1;
-      y1 = y0;
+    if (fabs(di) < floor_piv) di = di < 0.0 ? -floor_piv : floor_piv;
+    rd[n - 1] = 1.0 / di;
+    double sc = 1.0;  // scale of the right-hand side (1 / max of the previous iterate)
+    for (int iter = 0; iter < 2; ++iter) {
+      // L solve (the row interchanges applied as the factorisation made them)
+      double yi = iter == 0 ? 1.0 : y[0] * sc;
+  #pragma unroll 4
+      for (int i = 0; i < n - 1; ++i) {
+        const double yn = iter == 0 ? 1.0 : y[i + 1] * sc;
+        const bool sw = swp[i] != 0.0;
+        const double a = sw ? yn : yi, b = sw ? yi : yn;
+        y[i] = a;
+        yi = b - dl[i] * a;
+      }
+      // U solve (bandwidth 3)
+      double y1 = yi * rd[n - 1], y2 = 0.0;
+      y[n - 1] = y1;
+      double mx = fabs(y1);
+  #pragma unroll 4
+      for (int i = n - 2; i >= 0; --i) {
+        const double y0 = (y[i] - du[i] * y1 - du2[i] * y2) * rd[i];
+        y[i] = y0;
+        mx = fmax(mx, fabs(y0));
+        y2 = y1;
+        y1 = y0;
+      }
+      sc = 1.0 / mx;
     }
-    sc = 1.0 / mx;
+    double nrm = 0.0;
+  #pragma unroll 4
+    for (int i = 0; i < n; ++i) {
+      const double v = y[i] * sc;
+      y[i] = v;
+      nrm += v * v;
+    }
+    const double inv = 1.0 / sqrt(nrm);
+  #pragma unroll 4
+    for (int i = 0; i < n; ++i) y[i] *= inv;
+  } else {
+    double* __restrict__ dl = work;
+    double* __restrict__ rd = work + n;   // 1 / pivot
+    double* __restrict__ du = work + 2 * n;
+    double* __restrict__ du2 = work + 3 * n;
+    double* __restrict__ swp = work + 4 * n;
+    double scale = fabs(theta);
+  #pragma unroll 4
+    for (int i = 0; i < n; ++i) {
+      scale = fmax(scale, fabs(alpha[i]));
+      if (i < n - 1) scale = fmax(scale, fabs(beta[i]));
+    }
+    const double floor_piv = 1e-300 + 2.2e-16 * scale;
+    double di = alpha[0] - theta;          // current pivot candidate d_i
+    double dui = n > 1 ? beta[0] : 0.0;    // current super-diagonal du_i
+    // branch-free steps (selects instead of the two pivoting paths)
+    auto lu_step = [&](int i, double bi, double dn, double dun) {  // bi = dl_i, d_{i+1} and du_{i+1} before the step
+      const bool sw = !(fabs(di) >= fabs(bi));         // row interchange
+      const double dc = fabs(di) < floor_piv ? (di < 0.0 ? -floor_piv : floor_piv) : di;
+      const double r = 1.0 / (sw ? bi : dc);
+      const double f = (sw ? di : bi) * r;
+      dl[i] = f;
+      rd[i] = r;
+      du[i] = sw ? dn : dui;
+      du2[i] = sw ? dun : 0.0;
+      swp[i] = sw ? 1.0 : 0.0;
+      const double ndi = sw ? dui - f * dn : dn - f * dui;
+      dui = sw ? -f * dun : dun;
+      di = ndi;
+    };
+    int i = 0;
+    for (; i + G <= n - 1; i += G) {
+      double bv[G], dv[G], uv[G];
+  #pragma unroll
+      for (int t = 0; t < G; ++t) {
+        bv[t] = beta[i + t];
+        dv[t] = alpha[i + t + 1] - theta;
+        uv[t] = i + t < n - 2 ? beta[i + t + 1] : 0.0;
+      }
+  #pragma unroll
+      for (int t = 0; t < G; ++t) lu_step(i + t, bv[t], dv[t], uv[t]);
+    }
+    for (; i < n - 1; ++i) lu_step(i, beta[i], alpha[i + 1] - theta, i < n - 2 ? beta[i + 1] : 0.0);
+    if (fabs(di) < floor_piv) di = di < 0.0 ? -floor_piv : floor_piv;
+    rd[n - 1] = 1.0 / di;
+    double sc = 1.0;  // scale of the right-hand side (1 / max of the previous iterate)
+    for (int iter = 0; iter < 2; ++iter) {
+      // L solve (the row interchanges applied as the factorisation made them)
+      double yi = iter == 0 ? 1.0 : y[0] * sc;
+      auto l_step = [&](int i, double yn, double s, double l) {
+        const bool sw = s != 0.0;
+        const double a = sw ? yn : yi, b = sw ? yi : yn;
+        y[i] = a;
+        yi = b - l * a;
+      };
+      i = 0;
+      for (; i + G <= n - 1; i += G) {  // y[i + 1 ..] read before this group writes y[i ..]: the old values
+        double yv[G], sv[G], lv[G];
+  #pragma unroll
+        for (int t = 0; t < G; ++t) {
+          yv[t] = iter == 0 ? 1.0 : y[i + t + 1] * sc;
+          sv[t] = swp[i + t];
+          lv[t] = dl[i + t];
+        }
+  #pragma unroll
+        for (int t = 0; t < G; ++t) l_step(i + t, yv[t], sv[t], lv[t]);
+      }
+      for (; i < n - 1; ++i) l_step(i, iter == 0 ? 1.0 : y[i + 1] * sc, swp[i], dl[i]);
+      // U solve (bandwidth 3)
+      double y1 = yi * rd[n - 1], y2 = 0.0;
+      y[n - 1] = y1;
+      double mx = fabs(y1);
+      auto u_step = [&](int i, double yv, double u, double u2, double r) {
+        const double y0 = (yv - u * y1 - u2 * y2) * r;
+        y[i] = y0;
+        mx = fmax(mx, fabs(y0));
+        y2 = y1;
+        y1 = y0;
+      };
+      i = n - 2;
+      for (; i >= G - 1; i -= G) {  // steps i .. i - G + 1, all >= 0
+        double yv[G], uv[G], u2[G], rv[G];
+  #pragma unroll
+        for (int t = 0; t < G; ++t) {
+          yv[t] = y[i - t];
+          uv[t] = du[i - t];
+          u2[t] = du2[i - t];
+          rv[t] = rd[i - t];
+        }
+  #pragma unroll
+        for (int t = 0; t < G; ++t) u_step(i - t, yv[t], uv[t], u2[t], rv[t]);
+      }
+      for (; i >= 0; --i) u_step(i, y[i], du[i], du2[i], rd[i]);
+      sc = 1.0 / mx;
+    }
+    double nrm = 0.0;
+    i = 0;
+    for (; i + G <= n; i += G) {
+      double v[G];
+  #pragma unroll
+      for (int t = 0; t < G; ++t) v[t] = y[i + t] * sc;
+  #pragma unroll
+      for (int t = 0; t < G; ++t) {
+        y[i + t] = v[t];
+        nrm += v[t] * v[t];
+      }
+    }
+    for (; i < n; ++i) {
+      const double v = y[i] * sc;
+      y[i] = v;
+      nrm += v * v;
+    }
+    const double inv = 1.0 / sqrt(nrm);
+  #pragma unroll 4
+    for (int i = 0; i < n; ++i) y[i] *= inv;
   }
-  double nrm = 0.0;
-#pragma unroll 4
-  for (int i = 0; i < n; ++i) {
-    const double v = y[i] * sc;
-    y[i] = v;
-    nrm += v * v;
-  }
-  const double inv = 1.0 / sqrt(nrm);
-#pragma unroll 4
-  for (int i = 0; i < n; ++i) y[i] *= inv;
 }
 
 // Partial reorthogonalisation (Simon 1984): omega_{j+1,i} estimates q_{j+1}.q_i

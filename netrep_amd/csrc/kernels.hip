@@ -1731,7 +1731,7 @@ __device__ __forceinline__ void ritz_vector_wave(const double* __restrict__ Q, i
 // q_given: start from the vector the caller left in L.q (start_column's
 // G e_c*) instead of the near-constant one. gv_out: also leave G v in L.gv,
 // from the Lanczos relation (see the end of the function).
-template <int NW, bool BF, class MV>
+template <int NW, bool BF, class MV, int TRI_G = 8>
 __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, const LzLds& L, int* flags,
                                              double* Q, MV& mv, uint64_t& t_mark, bool* relax = nullptr,
                                              bool q_given = false, bool gv_out = false) {
@@ -1887,7 +1887,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
             // the Ritz coefficients by inverse iteration (the residual check's
             // backward recurrence is 2-4% faster but moved statistics by up to
             // 1.5e-10: profiles/r03/ritz_coefficients/)
-            tri_eigenvector(alpha, beta, j + 1, theta, ty, twork);
+            tri_eigenvector<TRI_G>(alpha, beta, j + 1, theta, ty, twork);
             NR_STAMP(12);  // Ritz coefficients (inverse iteration)
             L.h[0] = theta;  // for gv_out (h is idle once the run ends)
           }
@@ -2132,7 +2132,10 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       const bool q_given = PACKED && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
       NR_STAMP(8);  // start column
       const bool gv_rel = !dual;
-      lanczos_ritz<NW, PACKED>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr, q_given, gv_rel);
+      // (the large-module kernel keeps the tridiagonal eigenvector's previous
+      // loops: tri_eigenvector)
+      lanczos_ritz<NW, PACKED, decltype(mv), G64 ? 1 : 8>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr,
+                                                         q_given, gv_rel);
       relax = false;  // node contributions: the fp64 Gram
       if (!TABLE && dual) {
         profile_contrib_dual<NW>(P, k, m, Li, X, S, g1[0]);

@@ -509,7 +509,7 @@ __global__ void __launch_bounds__(EBS, 1) ek_kernel(EkParams P) {
       }
     }
     // Ritz coefficients (one lane), Ritz vector v = Q y, G v from the Lanczos relation
-    if (tid == 0) tri_eigenvector(alpha, beta, nsteps, theta, ty, part);
+    if (tid == 0) tri_eigenvector<8>(alpha, beta, nsteps, theta, ty, part);
     __syncthreads();
     EK_STAMP(8);
     double vt = 0.0;
