@@ -84,11 +84,11 @@ def test_bench_traffic_lookup_matches_committed_pmc():
     config, batch and kernel (profiles/pmc_traffic.json), as a [raw, x2] range
     with the pass's kernel time next to this run's (traffic_time_ratio)."""
     import bench
-    t = bench.traffic_fields("C3", 5120, "module_profile_kernel", 254.0, table=True)
+    t = bench.traffic_fields("C3", 5120, "module_profile_kernel", 247.3, table=True)
     assert t["traffic"] is not None and t["traffic"] > 0
     raw, x2 = t["traffic_range"]
     assert 0 < raw <= x2 == t["traffic"]
-    assert abs(t["traffic_time_ratio"] - 1.0) < 0.01     # the r06 final-tree pass: 253.79 ms
+    assert abs(t["traffic_time_ratio"] - 1.0) < 0.01     # the r06 final-tree pass: 247.90 ms
     # superseded rows (passes of kernels since replaced) are never reported
     assert bench.traffic_fields("C3", 256, "module_profile_kernel", 17.9)["traffic"] is None
     assert bench.traffic_fields("C3", 512, "module_profile_kernel", 1.0)["traffic"] is None
