@@ -1810,13 +1810,17 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     double* om_prev = omg + ((j + 2) % 3) * (mmax + 1);
     double* om_next = omg + ((j + 1) % 3) * (mmax + 1);
     anorm = fmax(anorm, fabs(alpha0) + sqrt(nb) + beta_prev);
+    bool reorth = false;  // one wave: decided in registers (omega_update's max is wave-uniform), no LDS round trip
     if (wave == 0) {  // alpha[j] passed in registers: no barrier before the recurrence
       const double mx = omega_update(alpha, beta, j, alpha0, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
-      if (lane == 0) s_reorth = force_next || mx > sqrt_eps;
+      if constexpr (NW == 1)
+        reorth = __builtin_amdgcn_readfirstlane((int)(force_next || mx > sqrt_eps)) != 0;  // a scalar branch
+      else if (lane == 0)
+        s_reorth = force_next || mx > sqrt_eps;
     }
     nr_sync<NW>();
     NR_STAMP(4);  // Lanczos: three-term step + omega recurrence
-    if (s_reorth) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
+    if (NW == 1 ? reorth : s_reorth != 0) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
       if constexpr (NW == 1)
         nb = reorthogonalise_wave(Q, k, j + 1, w, h);
       else
