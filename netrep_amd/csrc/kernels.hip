@@ -1731,7 +1731,10 @@ __device__ __forceinline__ void ritz_vector_wave(const double* __restrict__ Q, i
 // q_given: start from the vector the caller left in L.q (start_column's
 // G e_c*) instead of the near-constant one. gv_out: also leave G v in L.gv,
 // from the Lanczos relation (see the end of the function).
-template <int NW, bool BF, class MV, int TRI_G = 8>
+// BIG: the large-module kernel, whose register allocation is the tightest:
+// it keeps the previous loops of the tridiagonal eigenvector (the grouped
+// ones put spill code into its Gram loop).
+template <int NW, bool BF, class MV, bool BIG = false>
 __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, const LzLds& L, int* flags,
                                              double* Q, MV& mv, uint64_t& t_mark, bool* relax = nullptr,
                                              bool q_given = false, bool gv_out = false) {
@@ -1809,10 +1812,17 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     double* om_cur = omg + (j % 3) * (mmax + 1);
     double* om_prev = omg + ((j + 2) % 3) * (mmax + 1);
     double* om_next = omg + ((j + 1) % 3) * (mmax + 1);
-    anorm = fmax(anorm, fabs(alpha0) + sqrt(nb) + beta_prev);
+    // one wave: |w| and the q update's scale 1/|w| before the omega phase, off
+    // the chain after its fence (recomputed when the step reorthogonalises).
+    // C2's wave class -1.7%; the 4-wave table kernel measured +0.2% and keeps
+    // the previous order (profiles/r06/ab_inv/)
+    constexpr bool EARLY = NW == 1 && !BIG;
+    const double beta0 = sqrt(nb);
+    const double inv0 = EARLY ? 1.0 / beta0 : 0.0;
+    anorm = fmax(anorm, fabs(alpha0) + beta0 + beta_prev);
     bool reorth = false;  // one wave: decided in registers (omega_update's max is wave-uniform), no LDS round trip
     if (wave == 0) {  // alpha[j] passed in registers: no barrier before the recurrence
-      const double mx = omega_update(alpha, beta, j, alpha0, sqrt(nb), om_cur, om_prev, om_next, anorm, k, lane);
+      const double mx = omega_update(alpha, beta, j, alpha0, beta0, om_cur, om_prev, om_next, anorm, k, lane);
       if constexpr (NW == 1)
         reorth = __builtin_amdgcn_readfirstlane((int)(force_next || mx > sqrt_eps)) != 0;  // a scalar branch
       else if (lane == 0)
@@ -1820,7 +1830,8 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     }
     nr_sync<NW>();
     NR_STAMP(4);  // Lanczos: three-term step + omega recurrence
-    if (NW == 1 ? reorth : s_reorth != 0) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
+    const bool reorthed = NW == 1 ? reorth : s_reorth != 0;
+    if (reorthed) {  // reorthogonalise q_{j+1} against q_0..q_j, and the next one too
       if constexpr (NW == 1)
         nb = reorthogonalise_wave(Q, k, j + 1, w, h);
       else
@@ -1839,14 +1850,14 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
       if (P.diag && tid == 0) atomicAdd(P.diag + 3, 1);
     }
     NR_STAMP(9);  // Lanczos: reorthogonalisation
-    const double beta_j = sqrt(nb);
+    const double beta_j = !EARLY || reorthed ? sqrt(nb) : beta0;
     if (tid == 0) {
       alpha[j] = alpha_j;
       beta[j] = beta_j;
     }
     nsteps = j + 1;
     {  // next Lanczos vector (unused if this step's check ends the run), into the basis too
-      const double inv = 1.0 / beta_j;
+      const double inv = !EARLY || reorthed ? 1.0 / beta_j : inv0;
       double* qn = j + 1 < mcap ? Q + (int64_t)(j + 1) * k : nullptr;
       for (int c = tid; c < k; c += BS) {
         qprev[c] = q[c];
@@ -1891,7 +1902,7 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
             // the Ritz coefficients by inverse iteration (the residual check's
             // backward recurrence is 2-4% faster but moved statistics by up to
             // 1.5e-10: profiles/r03/ritz_coefficients/)
-            tri_eigenvector<TRI_G>(alpha, beta, j + 1, theta, ty, twork);
+            tri_eigenvector<BIG ? 1 : 8>(alpha, beta, j + 1, theta, ty, twork);
             NR_STAMP(12);  // Ritz coefficients (inverse iteration)
             L.h[0] = theta;  // for gv_out (h is idle once the run ends)
           }
@@ -2136,9 +2147,7 @@ __device__ __forceinline__ void profile_body(const ProfileParams& P) {
       const bool q_given = PACKED && start_column<NW>(G, G32, kc, n, L.q, L.w, part, kmax, L.red);
       NR_STAMP(8);  // start column
       const bool gv_rel = !dual;
-      // (the large-module kernel keeps the tridiagonal eigenvector's previous
-      // loops: tri_eigenvector)
-      lanczos_ritz<NW, PACKED, decltype(mv), G64 ? 1 : 8>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr,
+      lanczos_ritz<NW, PACKED, decltype(mv), G64>(P, n, L, s_flags, Q, mv, t_mark, G32 ? &relax : nullptr,
                                                          q_given, gv_rel);
       relax = false;  // node contributions: the fp64 Gram
       if (!TABLE && dual) {
