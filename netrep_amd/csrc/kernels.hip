@@ -1777,11 +1777,14 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   // geometric decay since the previous check predicts convergence (at most 8
   // steps on). Offline study on C3 null items (tools/sim_lanczos.py): 36.0
   // steps/item vs 37.9 for a fixed 8-step cadence, same number of checks.
-  // (the wave class checks first at step 20: its lone wave pays for every
-  // check's Sturm passes in full; C2 shape 1.908 -> 1.841 ms per 256
-  // permutations, 0.02% more steps. The 4-wave kernels keep 16: at C3, 20
-  // and 24 measured -0.2% and +0.9%, profiles/r05/firstcheck/)
-  constexpr int first_check = NW == 1 ? 20 : 16;
+  // (the wave class checks first at step 18: its lone wave pays for every
+  // check's Sturm passes in full; round 5 measured 20 against 16 on the C2
+  // shape, 1.908 -> 1.841 ms per 256 permutations; on round 6's cheaper
+  // checks, C2's profile kernel at 16 / 18 / 20 / 22 / 24: 24.69 / 24.24 /
+  // 24.87 / 25.41 / 25.61 ms per 5,120, profiles/r06/ab_firstcheck/. The
+  // 4-wave kernels keep 16: at C3, 20 and 24 measured -0.2% and +0.9%,
+  // profiles/r05/firstcheck/)
+  constexpr int first_check = NW == 1 ? 18 : 16;
   int next_check = mcap < first_check ? mcap : first_check;
   int prev_j = 0;  // lane 0 of wave 0 only
   double prev_r = 0.0;
@@ -1794,8 +1797,8 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     s_reorth = 0;
     flags[5] = 0;  // relaxed (fp32) matvecs
     // the next check is predicted to end the run: its eigenvalue to full
-    // precision in one go (the wave class's first check, at step 20, usually
-    // does: C2 items stop at ~24 steps)
+    // precision in one go (the wave class's first check: one stage measured
+    // faster on C2 than the coarse stage first, profiles/r06/ab_checks/)
     flags[6] = NW == 1;
   }
   for (int c = tid; c < k; c += BS) Q[c] = q[c];  // q_0 (later q_j are stored by the update below)
