@@ -1783,7 +1783,8 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
   // checks, C2's profile kernel at 16 / 18 / 20 / 22 / 24: 24.69 / 24.24 /
   // 24.87 / 25.41 / 25.61 ms per 5,120, profiles/r06/ab_firstcheck/. The
   // 4-wave kernels keep 16: at C3, 20 and 24 measured -0.2% and +0.9%,
-  // profiles/r05/firstcheck/)
+  // profiles/r05/firstcheck/; on the cheaper checks 18 and 20 +0.03% and
+  // +0.8%, profiles/r06/ab_firstcheck_c3/)
   constexpr int first_check = NW == 1 ? 18 : 16;
   int next_check = mcap < first_check ? mcap : first_check;
   int prev_j = 0;  // lane 0 of wave 0 only
