@@ -1798,9 +1798,10 @@ __device__ __forceinline__ void lanczos_ritz(const ProfileParams& P, int k, cons
     s_reorth = 0;
     flags[5] = 0;  // relaxed (fp32) matvecs
     // the next check is predicted to end the run: its eigenvalue to full
-    // precision in one go (the wave class's first check: one stage measured
-    // faster on C2 than the coarse stage first, profiles/r06/ab_checks/)
-    flags[6] = NW == 1;
+    // precision in one go. Not the first check (the wave class's, at step
+    // 20, was one stage: measured faster there, profiles/r06/ab_checks/; at
+    // step 18 the coarse stage first is 0.4% faster, profiles/r06/ab_coarse/)
+    flags[6] = 0;
   }
   for (int c = tid; c < k; c += BS) Q[c] = q[c];  // q_0 (later q_j are stored by the update below)
   for (int j = 0; j < mcap; ++j) {
